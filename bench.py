@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X-native reduction collective (BASELINE.json metric:
+"GiB/s device-resident float32 sum-reduce at 1/2/4/8 PEs vs HBM+xGMI roofline").
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mib 1024]
+
+N=1 (BASELINE configs[1]): ishmem_float_sum_reduce over a 1 GiB symmetric-heap array on one PE
+(reference semantics: dest = source, src/collectives/reduce_impl.h:288-289), plus the local
+combine unit dst = a + b (the per-step unit of the multi-PE path) at the same size.
+N>1 (launched by torch.distributed.run, one process per GPU): the same call over TEAM_WORLD =
+direct reduce-scatter + all-gather over xGMI (configs[2..3]); value = N * B / t (whole job).
+
+A "step" = one reduce of B bytes per PE, inputs already resident in HBM.  K steps are timed
+between barrier + device synchronize on both sides; ms_per_step is the max over ranks.  The
+dominant kernel's duration is measured with HIP events on the stream it runs on.  rank 0 at N=1
+also times the reference's host-proxy CPU reduce, restated in oracle/ (cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import uuid
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_LINK_GBS = 153.6       # per link, as given by the task brief (may be bidirectional)
+GiB = float(1 << 30)
+
+
+def pmc_traffic(kernel_tag: str, nbytes: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    f = ROOT / "profiles" / "pmc_summary.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        e = d.get(kernel_tag)
+        if e and int(e.get("payload_bytes", -1)) == nbytes:
+            return float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+    return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mib", type=int, default=1024, help="payload per PE in MiB (default 1 GiB)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-combine", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("bench.py --gpus N>1 must be launched by torch.distributed.run (one rank per GPU)")
+    dist = None
+    key = f"bench{uuid.uuid4().hex[:10]}"
+    if world > 1:
+        import torch.distributed as dist  # control plane only (gloo); the data path is ours
+        dist.init_process_group("gloo")
+        obj = [key]
+        dist.broadcast_object_list(obj, src=0)
+        key = obj[0]
+
+    import ishmem_amd as ish
+    from ishmem_amd import hip
+
+    ish.init(rank, world, local_rank, key)
+    n = (args.mib << 20) // 4
+    B = n * 4
+    src = ish.ishmem_malloc(B)
+    dst = ish.ishmem_malloc(B)
+    # Synthetic input with an exactly representable sum: x[i] = (i mod 1024) + pe.
+    pattern = (np.arange(n, dtype=np.int64) % 1024).astype(np.float32) + np.float32(rank)
+    hip.upload(src, pattern)
+    del pattern
+    stream = hip.stream_create()
+
+    def barrier():
+        hip.synchronize()
+        if dist is not None:
+            dist.barrier()
+        hip.synchronize()
+
+    def step():
+        r = ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, stream)
+        if r != 0:
+            raise RuntimeError(f"reduce failed: {ish.last_error()}")
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ev0, ev1 = hip.Event(), hip.Event()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    hip.stream_synchronize(stream)
+    t1 = time.perf_counter()
+    barrier()
+    wall_s = t1 - t0
+    kern_ms = ev0.elapsed_ms(ev1) / args.steps
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall_s, kern_ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall_s, kern_ms = float(t[0]), float(t[1])
+    if ish.lib().ishmemi_c_error_count():
+        raise RuntimeError("device barrier timeouts during the benchmark")
+
+    # Correctness of the timed buffers (sampled): dest = sum_pe((i mod 1024) + pe).
+    idx = np.random.default_rng(0).integers(0, n, 4096)
+    got = np.array([hip.download(dst + int(i) * 4, 1, np.float32)[0] for i in idx[:256]])
+    exp = (idx[:256] % 1024).astype(np.float32) * world + np.float32(world * (world - 1) / 2)
+    if not np.array_equal(got, exp):
+        raise RuntimeError("benchmark result check failed")
+
+    ms_per_step = wall_s * 1000.0 / args.steps
+    value = world * B / GiB / (ms_per_step / 1000.0)
+
+    if world == 1:
+        roof = {"bound": "hbm", "achieved": 2 * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "traffic": pmc_traffic("copy_1pe", B),
+                "kernel": "fanin_kernel<uint8,OR,vec> (1-PE reduce = copy, 2B per launch)"}
+    else:
+        link_bytes = 2.0 * (world - 1) / world * B  # RS + AG ingress per PE over p-1 links
+        roof = {"bound": "xgmi", "achieved": link_bytes / (kern_ms * 1e-3) / 1e9,
+                "peak": XGMI_LINK_GBS * (world - 1), "unit": "GB/s",
+                "traffic": pmc_traffic(f"allreduce_{world}pe", B),
+                "kernel": "allreduce_kernel<float,SUM,vec> (per-PE xGMI ingress 2(p-1)/p*B)"}
+    roof["frac"] = roof["achieved"] / roof["peak"]
+
+    extra = {}
+    if world == 1 and not args.no_combine:
+        # Local combine unit dst = a + b at the same size (3B HBM bytes per launch).
+        b2 = ish.ishmem_malloc(B)
+        hip.memcpy(b2, src, B)
+        for _ in range(3):
+            ish.combine("sum", "float", dst, [src, b2], n, stream)
+        e0, e1 = hip.Event(), hip.Event()
+        e0.record(stream)
+        for _ in range(args.steps):
+            ish.combine("sum", "float", dst, [src, b2], n, stream)
+        e1.record(stream)
+        hip.stream_synchronize(stream)
+        cms = e0.elapsed_ms(e1) / args.steps
+        ach = 3 * B / (cms * 1e-3) / 1e9
+        extra["combine"] = {"kernel": "fanin_kernel<float,SUM,vec> dst=a+b", "ms": cms,
+                            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("combine2_1pe", B)}
+        ish.ishmem_free(b2)
+
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        import oracle  # CPU baseline leg only: the reference's host-proxy reduce, restated
+        reps = 3
+        t_cpu = oracle.host_proxy_time(oracle.OPS["sum"], oracle.DTYPES["float"], n, 1, reps)
+        cpu = {"value": B / GiB / t_cpu, "unit": "GiB/s", "cores": 1, "kind": "port",
+               "sample": f"full workload: 1 PE f32 sum-reduce of {args.mib} MiB through 64 KiB host "
+                         f"bounce chunks (reduce_impl.h:186-228), best of {reps}"}
+
+    ish.ishmem_free(dst)
+    ish.ishmem_free(src)
+    hip.stream_destroy(stream)
+    ish.ishmem_finalize()
+    if rank == 0:
+        line = {
+            "metric": "GiB/s device-resident float32 sum-reduce at 1/2/4/8 PEs vs HBM+xGMI roofline",
+            "value": value, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"float32 sum-reduce, {args.mib} MiB per PE, {world} PE(s), "
+                                   f"symmetric-heap device buffers", "nreduce": n,
+                       "bytes_per_pe": B, "pes": world,
+                       "parallelism": "1 PE self-reduce" if world == 1 else f"direct RS+AG over {world} PEs"},
+            "kernel_ms": kern_ms, "roofline": roof, "cpu_baseline": cpu, **extra,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

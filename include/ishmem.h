@@ -1,0 +1,171 @@
+/* ishmem_amd — C++ API of the reduction-collective path with the reference's names.
+ *
+ * Source-compatible with the reduce section of oneapi-src/ishmem's public header
+ * (src/ishmem.h:923-1238) and its setup calls (src/ishmem.h:40-86, :1555-1559): every
+ *   int ishmem_<TYPENAME>_<op>_reduce([ishmem_team_t team,] TYPE *dest, const TYPE *source,
+ *                                      size_t nreduce)
+ * and the generic  template <typename T> int ishmem_<op>_reduce([team,] T*, const T*, size_t)
+ * are header-only inline wrappers over the C-ABI in ishmem_capi.h (link -lishmem_amd).
+ * TYPENAME x op matrix = src/collectives/reduce.cpp:95-417 (bitwise ops on unsigned and
+ * fixed-width integer types only; schar bitwise is declared by the reference but never defined,
+ * reduce.cpp:97-110, so it is not provided here either).
+ *
+ * Host-callable only: the reference's device-callable overloads (SYCL_EXTERNAL) are replaced by
+ * kernels the library launches itself; see ishmemx.h for the stream-ordered variant.
+ */
+#ifndef ISHMEM_AMD_ISHMEM_H
+#define ISHMEM_AMD_ISHMEM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "ishmem_capi.h"
+
+typedef int ishmem_team_t; /* src/ishmem.h:61 */
+#define ISHMEM_TEAM_INVALID ISHMEMI_C_TEAM_INVALID
+#define ISHMEM_TEAM_WORLD   ISHMEMI_C_TEAM_WORLD
+#define ISHMEM_TEAM_SHARED  ISHMEMI_C_TEAM_SHARED
+
+/* ---- setup (src/ishmem.h:40-56) ---------------------------------------------------------- */
+inline void ishmem_init(void) { (void) ishmemi_c_init(); }
+inline void ishmem_finalize(void) { (void) ishmemi_c_finalize(); }
+inline int ishmem_my_pe(void) { return ishmemi_c_my_pe(); }
+inline int ishmem_n_pes(void) { return ishmemi_c_n_pes(); }
+inline void *ishmem_malloc(size_t size) { return ishmemi_c_malloc(size); }
+inline void *ishmem_align(size_t alignment, size_t size) { return ishmemi_c_align(alignment, size); }
+inline void *ishmem_calloc(size_t count, size_t size) { return ishmemi_c_calloc(count, size); }
+inline void ishmem_free(void *ptr) { ishmemi_c_free(ptr); }
+inline void *ishmem_ptr(const void *dest, int pe) { return ishmemi_c_ptr(dest, pe); }
+
+/* ---- teams (src/ishmem.h:74-86) ---------------------------------------------------------- */
+inline int ishmem_team_my_pe(ishmem_team_t team) { return ishmemi_c_team_my_pe(team); }
+inline int ishmem_team_n_pes(ishmem_team_t team) { return ishmemi_c_team_n_pes(team); }
+inline int ishmem_team_translate_pe(ishmem_team_t src_team, int src_pe, ishmem_team_t dest_team)
+{
+    return ishmemi_c_team_translate_pe(src_team, src_pe, dest_team);
+}
+/* The reference's config/config_mask arguments (src/ishmem.h:79-85) are accepted and ignored:
+ * no team configuration option affects reductions. */
+inline int ishmem_team_split_strided(ishmem_team_t parent_team, int start, int stride, int size,
+                                     const void * /*config*/, long /*config_mask*/,
+                                     ishmem_team_t *new_team)
+{
+    return ishmemi_c_team_split_strided(parent_team, start, stride, size, new_team);
+}
+inline void ishmem_team_destroy(ishmem_team_t team) { ishmemi_c_team_destroy(team); }
+
+/* ---- synchronisation (src/ishmem.h:1555-1559) -------------------------------------------- */
+inline void ishmem_barrier_all(void) { (void) ishmemi_c_barrier_all(); }
+inline void ishmem_sync_all(void) { (void) ishmemi_c_sync_all(); }
+inline int ishmem_team_sync(ishmem_team_t team) { return ishmemi_c_team_sync(team); }
+
+/* ---- reductions ---------------------------------------------------------------------------- */
+namespace ishmemi_cxx {
+/* C type -> canonical dtype (the reference's ishmemi_union_get_base_type, src/ishmem/util.h:452-479) */
+template <typename T>
+constexpr int dtype_of()
+{
+    static_assert(std::is_arithmetic_v<T> && sizeof(T) <= 8, "unsupported reduction type");
+    if constexpr (std::is_same_v<T, float>) return ISHMEMI_DT_FLOAT;
+    else if constexpr (std::is_same_v<T, double>) return ISHMEMI_DT_DOUBLE;
+    else if constexpr (std::is_signed_v<T>)
+        return sizeof(T) == 1 ? ISHMEMI_DT_INT8 : sizeof(T) == 2 ? ISHMEMI_DT_INT16
+               : sizeof(T) == 4 ? ISHMEMI_DT_INT32 : ISHMEMI_DT_INT64;
+    else
+        return sizeof(T) == 1 ? ISHMEMI_DT_UINT8 : sizeof(T) == 2 ? ISHMEMI_DT_UINT16
+               : sizeof(T) == 4 ? ISHMEMI_DT_UINT32 : ISHMEMI_DT_UINT64;
+}
+template <typename T>
+inline int reduce(ishmem_team_t team, int op, T *dest, const T *source, size_t nreduce)
+{
+    return ishmemi_c_reduce(team, op, dtype_of<T>(), (void *) dest, (const void *) source, nreduce);
+}
+}  // namespace ishmemi_cxx
+
+#define ISHMEMI_CXX_GENERIC(OPNAME, OPC)                                                            \
+    template <typename T>                                                                          \
+    inline int ishmem_##OPNAME##_reduce(T *dest, const T *source, size_t nreduce)                  \
+    {                                                                                              \
+        return ishmemi_cxx::reduce<T>(ISHMEM_TEAM_WORLD, OPC, dest, source, nreduce);              \
+    }                                                                                              \
+    template <typename T>                                                                          \
+    inline int ishmem_##OPNAME##_reduce(ishmem_team_t team, T *dest, const T *source,              \
+                                        size_t nreduce)                                            \
+    {                                                                                              \
+        return ishmemi_cxx::reduce<T>(team, OPC, dest, source, nreduce);                           \
+    }
+
+ISHMEMI_CXX_GENERIC(and, ISHMEMI_OP_AND)
+ISHMEMI_CXX_GENERIC(or, ISHMEMI_OP_OR)
+ISHMEMI_CXX_GENERIC(xor, ISHMEMI_OP_XOR)
+ISHMEMI_CXX_GENERIC(max, ISHMEMI_OP_MAX)
+ISHMEMI_CXX_GENERIC(min, ISHMEMI_OP_MIN)
+ISHMEMI_CXX_GENERIC(sum, ISHMEMI_OP_SUM)
+ISHMEMI_CXX_GENERIC(prod, ISHMEMI_OP_PROD)
+
+#define ISHMEMI_CXX_TYPED(TYPENAME, TYPE, OPNAME, OPC)                                              \
+    inline int ishmem_##TYPENAME##_##OPNAME##_reduce(TYPE *dest, const TYPE *source,               \
+                                                     size_t nreduce)                               \
+    {                                                                                              \
+        return ishmemi_cxx::reduce<TYPE>(ISHMEM_TEAM_WORLD, OPC, dest, source, nreduce);           \
+    }                                                                                              \
+    inline int ishmem_##TYPENAME##_##OPNAME##_reduce(ishmem_team_t team, TYPE *dest,               \
+                                                     const TYPE *source, size_t nreduce)           \
+    {                                                                                              \
+        return ishmemi_cxx::reduce<TYPE>(team, OPC, dest, source, nreduce);                        \
+    }
+
+/* bitwise: src/collectives/reduce.cpp:95-147, :257-309 */
+#define ISHMEMI_CXX_BITWISE_TYPES(X, OPNAME, OPC)                                                   \
+    X(uchar, unsigned char, OPNAME, OPC)                                                           \
+    X(ushort, unsigned short, OPNAME, OPC)                                                         \
+    X(uint, unsigned int, OPNAME, OPC)                                                             \
+    X(ulong, unsigned long, OPNAME, OPC)                                                           \
+    X(ulonglong, unsigned long long, OPNAME, OPC)                                                  \
+    X(int8, int8_t, OPNAME, OPC)                                                                   \
+    X(int16, int16_t, OPNAME, OPC)                                                                 \
+    X(int32, int32_t, OPNAME, OPC)                                                                 \
+    X(int64, int64_t, OPNAME, OPC)                                                                 \
+    X(uint8, uint8_t, OPNAME, OPC)                                                                 \
+    X(uint16, uint16_t, OPNAME, OPC)                                                               \
+    X(uint32, uint32_t, OPNAME, OPC)                                                               \
+    X(uint64, uint64_t, OPNAME, OPC)                                                               \
+    X(size, size_t, OPNAME, OPC)
+
+/* max/min/sum/prod: src/collectives/reduce.cpp:149-255, :311-417 */
+#define ISHMEMI_CXX_ARITH_TYPES(X, OPNAME, OPC)                                                     \
+    X(char, char, OPNAME, OPC)                                                                     \
+    X(schar, signed char, OPNAME, OPC)                                                             \
+    X(short, short, OPNAME, OPC)                                                                   \
+    X(int, int, OPNAME, OPC)                                                                       \
+    X(long, long, OPNAME, OPC)                                                                     \
+    X(longlong, long long, OPNAME, OPC)                                                            \
+    X(ptrdiff, ptrdiff_t, OPNAME, OPC)                                                             \
+    X(uchar, unsigned char, OPNAME, OPC)                                                           \
+    X(ushort, unsigned short, OPNAME, OPC)                                                         \
+    X(uint, unsigned int, OPNAME, OPC)                                                             \
+    X(ulong, unsigned long, OPNAME, OPC)                                                           \
+    X(ulonglong, unsigned long long, OPNAME, OPC)                                                  \
+    X(int8, int8_t, OPNAME, OPC)                                                                   \
+    X(int16, int16_t, OPNAME, OPC)                                                                 \
+    X(int32, int32_t, OPNAME, OPC)                                                                 \
+    X(int64, int64_t, OPNAME, OPC)                                                                 \
+    X(uint8, uint8_t, OPNAME, OPC)                                                                 \
+    X(uint16, uint16_t, OPNAME, OPC)                                                               \
+    X(uint32, uint32_t, OPNAME, OPC)                                                               \
+    X(uint64, uint64_t, OPNAME, OPC)                                                               \
+    X(size, size_t, OPNAME, OPC)                                                                   \
+    X(float, float, OPNAME, OPC)                                                                   \
+    X(double, double, OPNAME, OPC)
+
+ISHMEMI_CXX_BITWISE_TYPES(ISHMEMI_CXX_TYPED, and, ISHMEMI_OP_AND)
+ISHMEMI_CXX_BITWISE_TYPES(ISHMEMI_CXX_TYPED, or, ISHMEMI_OP_OR)
+ISHMEMI_CXX_BITWISE_TYPES(ISHMEMI_CXX_TYPED, xor, ISHMEMI_OP_XOR)
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_TYPED, max, ISHMEMI_OP_MAX)
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_TYPED, min, ISHMEMI_OP_MIN)
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_TYPED, sum, ISHMEMI_OP_SUM)
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_TYPED, prod, ISHMEMI_OP_PROD)
+
+#endif /* ISHMEM_AMD_ISHMEM_H */

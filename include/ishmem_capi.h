@@ -1,0 +1,153 @@
+/* ishmem_amd — C-ABI of the MI355X-native reduction-collective path.
+ *
+ * This is the drop-in boundary: plain C types, plain pointers and sizes, no torch/HIP types in
+ * the signatures (streams are passed as `void *` = hipStream_t).  The C++ API with the
+ * reference's exact names (include/ishmem.h, include/ishmemx.h) is a header-only layer of
+ * inline wrappers over these entry points, so a maintainer can bind this library from any
+ * language that speaks the C ABI (ctypes / cffi / JNI).
+ *
+ * Every function returns 0 on success and nonzero on failure (reference convention:
+ * src/ishmem/err.h, collectives return int 0/!=0, src/collectives/reduce_impl.h:259-317);
+ * pointer-returning functions return NULL on failure.  Nothing throws across this ABI.
+ * ishmemi_c_last_error() returns a human-readable reason for the last failure of this thread.
+ *
+ * Citations are reference paths (oneapi-src/ishmem v1.5.1) of the interface each entry replaces.
+ */
+#ifndef ISHMEM_AMD_CAPI_H
+#define ISHMEM_AMD_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Reduction operators — relative order of AND_REDUCE..PROD_REDUCE in src/ishmem/types.h:66-72. */
+typedef enum {
+    ISHMEMI_OP_AND = 0,
+    ISHMEMI_OP_OR = 1,
+    ISHMEMI_OP_XOR = 2,
+    ISHMEMI_OP_MAX = 3,
+    ISHMEMI_OP_MIN = 4,
+    ISHMEMI_OP_SUM = 5,
+    ISHMEMI_OP_PROD = 6,
+    ISHMEMI_OP_COUNT = 7
+} ishmemi_c_op_t;
+
+/* Canonical fixed-width element types (the reference canonicalises every C type to these before
+ * combining: src/collectives/reduce_impl.h:22-59, src/ishmem/util.h:452-479). */
+typedef enum {
+    ISHMEMI_DT_INT8 = 0,
+    ISHMEMI_DT_INT16 = 1,
+    ISHMEMI_DT_INT32 = 2,
+    ISHMEMI_DT_INT64 = 3,
+    ISHMEMI_DT_UINT8 = 4,
+    ISHMEMI_DT_UINT16 = 5,
+    ISHMEMI_DT_UINT32 = 6,
+    ISHMEMI_DT_UINT64 = 7,
+    ISHMEMI_DT_FLOAT = 8,
+    ISHMEMI_DT_DOUBLE = 9,
+    ISHMEMI_DT_COUNT = 10
+} ishmemi_c_dtype_t;
+
+/* Team handles — src/ishmem.h:61-72 (ISHMEM_TEAM_WORLD 0, ISHMEM_TEAM_SHARED 1) and
+ * src/ishmemx.h:11 (ISHMEMX_TEAM_NODE 2).  On one MI355X node all three span every PE. */
+#define ISHMEMI_C_TEAM_INVALID (-1)
+#define ISHMEMI_C_TEAM_WORLD 0
+#define ISHMEMI_C_TEAM_SHARED 1
+#define ISHMEMI_C_TEAM_NODE 2
+
+/* ---- lifecycle — replaces ishmem_init / ishmem_finalize (src/ishmem.h:40-41,
+ *      src/ishmem.cpp:224-407) and ishmemx_init_attr (src/ishmemx.h:21-37) ---------------------
+ * ishmemi_c_init(): PE identity from the environment: ISHMEM_PE / ISHMEM_NPES, else the
+ *   torchrun variables RANK / WORLD_SIZE; device from ISHMEM_DEVICE, else LOCAL_RANK, else 0;
+ *   bootstrap key from ISHMEM_BOOTSTRAP_KEY, else derived from MASTER_PORT.
+ * ishmemi_c_init_pe(): the same with explicit values (device < 0: keep the env rule).
+ * The bootstrap (handle exchange + host barrier) is a POSIX shared-memory segment on the node;
+ * it replaces the reference's MPI/OpenSHMEM/PMI runtime (src/runtime.h:22-84) for the only job
+ * it does on this path: exchanging the heap IPC handles (src/ipc.cpp:123-233). */
+int ishmemi_c_init(void);
+int ishmemi_c_init_pe(int pe, int npes, int device, const char *bootstrap_key);
+int ishmemi_c_finalize(void);
+int ishmemi_c_initialized(void);
+int ishmemi_c_my_pe(void);  /* ishmem_my_pe, src/ishmem.h:54 */
+int ishmemi_c_n_pes(void);  /* ishmem_n_pes, src/ishmem.h:55 */
+int ishmemi_c_device(void); /* HIP device ordinal this PE runs on */
+
+/* ---- symmetric heap in HBM — replaces ishmem_malloc/align/calloc/free (src/ishmem.h:48-51,
+ *      src/memory.cpp:200-300) and ishmem_ptr (src/ishmem.h:56) -----------------------------
+ * One hipMalloc'd heap per PE (size: ISHMEM_SYMMETRIC_SIZE, src/ishmem/env_defs.h:20), mapped
+ * into every peer by HIP IPC.  Allocation is collective and deterministic (same offsets on every
+ * PE).  ishmemi_c_ptr returns the address of `dest` on PE `pe` in this process (NULL if `dest`
+ * is not in the heap). */
+void *ishmemi_c_malloc(size_t size);
+void *ishmemi_c_align(size_t alignment, size_t size);
+void *ishmemi_c_calloc(size_t count, size_t size);
+void ishmemi_c_free(void *ptr);
+void *ishmemi_c_ptr(const void *dest, int pe);
+int ishmemi_c_heap_info(void **base, size_t *size, size_t *used);
+
+/* ---- teams — src/ishmem.h:74-86 ------------------------------------------------------------ */
+int ishmemi_c_team_my_pe(int team);
+int ishmemi_c_team_n_pes(int team);
+int ishmemi_c_team_translate_pe(int src_team, int src_pe, int dest_team);
+int ishmemi_c_team_split_strided(int parent_team, int start, int stride, int size, int *new_team);
+void ishmemi_c_team_destroy(int team);
+
+/* ---- synchronisation — ishmem_barrier_all / sync_all / team_sync (src/ishmem.h:1555-1559,
+ *      device implementation src/collectives/sync_impl.h:30-69) --------------------------------- */
+int ishmemi_c_barrier_all(void);
+int ishmemi_c_sync_all(void);
+int ishmemi_c_team_sync(int team);
+
+/* ---- THE HOT PATH ----------------------------------------------------------------------------
+ * ishmemi_c_reduce: blocking reduction over a team.  Replaces every
+ *   int ishmem_<TYPENAME>_<op>_reduce([ishmem_team_t team,] TYPE *dest, const TYPE *source,
+ *                                     size_t nreduce)
+ * (src/ishmem.h:923-1238, instantiated in src/collectives/reduce.cpp:8-417) whose body is
+ * ishmemi_reduce<T,OP>(team, dest, source, nreduce) (src/collectives/reduce_impl.h:259-317).
+ * `dest`/`source`: symmetric-heap device memory (device path), or any device / host memory
+ * (staged through the heap).  `source == dest` (in place) or disjoint, as the reference requires
+ * (docs/source/collectives.rst:1025-1028).  Returns when `dest` holds the result on this PE and
+ * `source` may be reused (collectives.rst:1046-1050).
+ *
+ * ishmemi_c_reduce_on_stream: the HIP-stream analogue of
+ *   sycl::event ishmemx_<TYPENAME>_<op>_reduce_on_queue(..., int *ret, sycl::queue &q, deps)
+ * (src/ishmemx.h:1172-1803, src/collectives/reduce_impl.h:444-474): enqueues the collective on
+ * `stream` (hipStream_t) and returns at once; the kernel writes 0 to *ret (device-visible int,
+ * may be NULL) on success (reduce_impl.h:461-463). */
+int ishmemi_c_reduce(int team, int op, int dtype, void *dest, const void *source, size_t nreduce);
+int ishmemi_c_reduce_on_stream(int team, int op, int dtype, void *dest, const void *source,
+                               size_t nreduce, int *ret, void *stream);
+
+/* Local combine unit of the path (what one reduce step does per element):
+ *   dst[i] = op(srcs[0][i], srcs[1][i], ..., srcs[nsrc-1][i]), folded in source order.
+ * Replaces vector_reduce / vector_reduce_work_group (src/collectives/reduce_impl.h:105-183).
+ * Device pointers; asynchronous on `stream`. nsrc in 1..16. */
+int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n,
+                      void *stream);
+
+/* ---- diagnostics / parameters ----------------------------------------------------------------
+ * ishmemi_c_set_param names: "max_blocks" (workgroups per collective launch, <= 1024),
+ * "timeout_ms" (bound on every device-side spin), "debug". */
+const char *ishmemi_c_last_error(void);
+int ishmemi_c_set_param(const char *name, long long value);
+long long ishmemi_c_get_param(const char *name);
+/* Number of collective launches whose device-side barriers timed out since init. */
+int ishmemi_c_error_count(void);
+/* Bytes of one element of `dtype` (0 if invalid); 1 if (op, dtype) is a valid pair. */
+size_t ishmemi_c_dtype_size(int dtype);
+int ishmemi_c_op_dtype_valid(int op, int dtype);
+/* Partition used by the multi-PE schedule: items of member `c` out of `nitems` (test hook). */
+int ishmemi_c_chunk_bounds(uint64_t nitems, int npes, int c, uint64_t *begin, uint64_t *end);
+/* Native bootstrap self-test (no GPU needed): allgather of one int per PE + barrier.
+ * Fills out[npes]; used by the multi-process CPU tests. */
+int ishmemi_c_bootstrap_selftest(int pe, int npes, const char *key, int value, int *out);
+const char *ishmemi_c_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ISHMEM_AMD_CAPI_H */

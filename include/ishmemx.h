@@ -1,0 +1,58 @@
+/* ishmem_amd — extension API of the reduction path (reference: src/ishmemx.h).
+ *
+ * The reference's queue-ordered variant
+ *   sycl::event ishmemx_<TYPENAME>_<op>_reduce_on_queue([team,] dest, source, nreduce, int *ret,
+ *                                                       sycl::queue &q, deps = {})
+ * (src/ishmemx.h:1172-1803, src/collectives/reduce_impl.h:444-474) becomes the HIP-stream
+ * variant below: enqueue on `stream`, return immediately (0 = enqueued), the kernel stores 0 into
+ * *ret (device-visible int, may be nullptr) when the collective completed successfully.
+ * Dependencies are expressed by stream order / hipStreamWaitEvent instead of `deps`.
+ */
+#ifndef ISHMEM_AMD_ISHMEMX_H
+#define ISHMEM_AMD_ISHMEMX_H
+
+#include "ishmem.h"
+
+#define ISHMEMX_TEAM_NODE ISHMEMI_C_TEAM_NODE /* src/ishmemx.h:11 */
+
+typedef struct ihipStream_t *hipStream_t; /* identical to HIP's own typedef */
+
+namespace ishmemi_cxx {
+template <typename T>
+inline int reduce_on_stream(ishmem_team_t team, int op, T *dest, const T *source, size_t nreduce,
+                            int *ret, hipStream_t stream)
+{
+    return ishmemi_c_reduce_on_stream(team, op, dtype_of<T>(), (void *) dest, (const void *) source,
+                                      nreduce, ret, (void *) stream);
+}
+}  // namespace ishmemi_cxx
+
+#define ISHMEMI_CXX_ON_STREAM(TYPENAME, TYPE, OPNAME, OPC)                                          \
+    inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_on_stream(                                   \
+        TYPE *dest, const TYPE *source, size_t nreduce, int *ret, hipStream_t stream)              \
+    {                                                                                              \
+        return ishmemi_cxx::reduce_on_stream<TYPE>(ISHMEM_TEAM_WORLD, OPC, dest, source, nreduce,  \
+                                                   ret, stream);                                   \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_on_stream(                                   \
+        ishmem_team_t team, TYPE *dest, const TYPE *source, size_t nreduce, int *ret,              \
+        hipStream_t stream)                                                                        \
+    {                                                                                              \
+        return ishmemi_cxx::reduce_on_stream<TYPE>(team, OPC, dest, source, nreduce, ret, stream); \
+    }
+
+ISHMEMI_CXX_BITWISE_TYPES(ISHMEMI_CXX_ON_STREAM, and, ISHMEMI_OP_AND)
+ISHMEMI_CXX_BITWISE_TYPES(ISHMEMI_CXX_ON_STREAM, or, ISHMEMI_OP_OR)
+ISHMEMI_CXX_BITWISE_TYPES(ISHMEMI_CXX_ON_STREAM, xor, ISHMEMI_OP_XOR)
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, max, ISHMEMI_OP_MAX)
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, min, ISHMEMI_OP_MIN)
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, sum, ISHMEMI_OP_SUM)
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, prod, ISHMEMI_OP_PROD)
+
+/* Explicit-identity init (the role of ishmemx_init_attr, src/ishmemx.h:21-37). */
+inline int ishmemx_init_pe(int pe, int npes, int device, const char *bootstrap_key)
+{
+    return ishmemi_c_init_pe(pe, npes, device, bootstrap_key);
+}
+
+#endif /* ISHMEM_AMD_ISHMEMX_H */

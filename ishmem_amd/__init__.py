@@ -1,0 +1,227 @@
+"""ishmem_amd — MI355X-native reduction collective with the ishmem API surface.
+
+Python host mirror of the reference's reduce interface (oneapi-src/ishmem v1.5.1,
+src/ishmem.h:923-1238, src/ishmemx.h:1172-1803) over the C-ABI in include/ishmem_capi.h.
+Names, argument meaning and error behaviour follow the reference: every
+``ishmem_<TYPENAME>_<op>_reduce([team,] dest, source, nreduce)`` returns 0 on success and
+nonzero on failure (``last_error()`` says why); ``dest``/``source`` are device addresses (ints)
+from ``ishmem_malloc`` (symmetric heap) or any device / host address.
+
+The work is done by ishmem_amd/libishmem_amd.so (HIP kernels for gfx950).  There is no Python
+or CPU fallback: importing this package fails if the native library cannot be loaded.
+"""
+from __future__ import annotations
+
+import ctypes
+import sys
+
+from ._lib import LIB_PATH, load
+
+_L = load()
+
+# ---- enums (include/ishmem_capi.h) -------------------------------------------------------
+OPS = {"and": 0, "or": 1, "xor": 2, "max": 3, "min": 4, "sum": 5, "prod": 6}
+DTYPES = {"int8": 0, "int16": 1, "int32": 2, "int64": 3, "uint8": 4, "uint16": 5,
+          "uint32": 6, "uint64": 7, "float": 8, "double": 9}
+ISHMEM_TEAM_INVALID = -1
+ISHMEM_TEAM_WORLD = 0
+ISHMEM_TEAM_SHARED = 1
+ISHMEMX_TEAM_NODE = 2
+
+# Reference TYPENAME -> canonical fixed-width type (x86-64 / gfx950 LP64, char signed).
+# Instantiation lists: src/collectives/reduce.cpp:95-417.
+TYPENAMES = {
+    "char": "int8", "schar": "int8", "short": "int16", "int": "int32", "long": "int64",
+    "longlong": "int64", "ptrdiff": "int64", "uchar": "uint8", "ushort": "uint16",
+    "uint": "uint32", "ulong": "uint64", "ulonglong": "uint64", "int8": "int8",
+    "int16": "int16", "int32": "int32", "int64": "int64", "uint8": "uint8", "uint16": "uint16",
+    "uint32": "uint32", "uint64": "uint64", "size": "uint64", "float": "float", "double": "double",
+}
+BITWISE_TYPENAMES = ["uchar", "ushort", "uint", "ulong", "ulonglong", "int8", "int16", "int32",
+                     "int64", "uint8", "uint16", "uint32", "uint64", "size"]
+ARITH_TYPENAMES = ["char", "schar", "short", "int", "long", "longlong", "ptrdiff", "uchar",
+                   "ushort", "uint", "ulong", "ulonglong", "int8", "int16", "int32", "int64",
+                   "uint8", "uint16", "uint32", "uint64", "size", "float", "double"]
+TYPENAMES_FOR_OP = {**{op: BITWISE_TYPENAMES for op in ("and", "or", "xor")},
+                    **{op: ARITH_TYPENAMES for op in ("max", "min", "sum", "prod")}}
+
+
+def lib() -> ctypes.CDLL:
+    return _L
+
+
+def last_error() -> str:
+    e = _L.ishmemi_c_last_error()
+    return e.decode() if e else ""
+
+
+def version() -> str:
+    return _L.ishmemi_c_version().decode()
+
+
+# ---- lifecycle ---------------------------------------------------------------------------
+def ishmem_init() -> None:
+    """ishmem_init (src/ishmem.h:40): PE identity from ISHMEM_PE/ISHMEM_NPES or RANK/WORLD_SIZE."""
+    if _L.ishmemi_c_init() != 0:
+        raise RuntimeError(f"ishmem_init failed: {last_error()}")
+
+
+def init(pe: int = 0, npes: int = 1, device: int = -1, key: str | None = None) -> None:
+    """Explicit-identity init (ishmemx_init_attr analogue, src/ishmemx.h:21-37)."""
+    if _L.ishmemi_c_init_pe(pe, npes, device, (key or "").encode()) != 0:
+        raise RuntimeError(f"ishmem init failed: {last_error()}")
+
+
+def ishmem_finalize() -> None:
+    _L.ishmemi_c_finalize()
+
+
+finalize = ishmem_finalize
+
+
+def initialized() -> bool:
+    return bool(_L.ishmemi_c_initialized())
+
+
+def ishmem_my_pe() -> int:
+    return _L.ishmemi_c_my_pe()
+
+
+def ishmem_n_pes() -> int:
+    return _L.ishmemi_c_n_pes()
+
+
+# ---- symmetric heap ----------------------------------------------------------------------
+def ishmem_malloc(size: int) -> int:
+    p = _L.ishmemi_c_malloc(size)
+    if not p:
+        raise MemoryError(f"ishmem_malloc({size}) failed: {last_error()}")
+    return p
+
+
+def ishmem_align(alignment: int, size: int) -> int:
+    p = _L.ishmemi_c_align(alignment, size)
+    if not p:
+        raise MemoryError(f"ishmem_align failed: {last_error()}")
+    return p
+
+
+def ishmem_calloc(count: int, size: int) -> int:
+    p = _L.ishmemi_c_calloc(count, size)
+    if not p:
+        raise MemoryError(f"ishmem_calloc failed: {last_error()}")
+    return p
+
+
+def ishmem_free(ptr: int) -> None:
+    _L.ishmemi_c_free(ptr)
+
+
+def ishmem_ptr(dest: int, pe: int) -> int | None:
+    return _L.ishmemi_c_ptr(dest, pe)
+
+
+# ---- teams / sync ------------------------------------------------------------------------
+def ishmem_team_my_pe(team: int) -> int:
+    return _L.ishmemi_c_team_my_pe(team)
+
+
+def ishmem_team_n_pes(team: int) -> int:
+    return _L.ishmemi_c_team_n_pes(team)
+
+
+def ishmem_team_translate_pe(src_team: int, src_pe: int, dest_team: int) -> int:
+    return _L.ishmemi_c_team_translate_pe(src_team, src_pe, dest_team)
+
+
+def ishmem_team_split_strided(parent: int, start: int, stride: int, size: int) -> tuple[int, int]:
+    """Returns (status, new_team) — new_team is ISHMEM_TEAM_INVALID on non-members."""
+    t = ctypes.c_int(-1)
+    r = _L.ishmemi_c_team_split_strided(parent, start, stride, size, ctypes.byref(t))
+    return r, t.value
+
+
+def ishmem_team_destroy(team: int) -> None:
+    _L.ishmemi_c_team_destroy(team)
+
+
+def ishmem_barrier_all() -> int:
+    return _L.ishmemi_c_barrier_all()
+
+
+def ishmem_sync_all() -> int:
+    return _L.ishmemi_c_sync_all()
+
+
+def ishmem_team_sync(team: int) -> int:
+    return _L.ishmemi_c_team_sync(team)
+
+
+def set_param(name: str, value: int) -> int:
+    return _L.ishmemi_c_set_param(name.encode(), int(value))
+
+
+def get_param(name: str) -> int:
+    return int(_L.ishmemi_c_get_param(name.encode()))
+
+
+# ---- the reduction path ------------------------------------------------------------------
+def reduce(op: str, dtype: str, dest: int, source: int, nreduce: int, team: int = ISHMEM_TEAM_WORLD) -> int:
+    """ishmemi_reduce<T,OP>(team, dest, source, nreduce) (src/collectives/reduce_impl.h:259-317)."""
+    return _L.ishmemi_c_reduce(team, OPS[op], DTYPES[dtype], dest, source, nreduce)
+
+
+def reduce_on_stream(op: str, dtype: str, dest: int, source: int, nreduce: int, ret: int | None,
+                     stream: int, team: int = ISHMEM_TEAM_WORLD) -> int:
+    """ishmemx_*_reduce_on_queue analogue (src/collectives/reduce_impl.h:444-474)."""
+    return _L.ishmemi_c_reduce_on_stream(team, OPS[op], DTYPES[dtype], dest, source, nreduce,
+                                         ret or None, stream or None)
+
+
+def combine(op: str, dtype: str, dst: int, srcs: list[int], n: int, stream: int = 0) -> int:
+    """Local combine unit dst = op(srcs...) (vector_reduce, reduce_impl.h:105-183)."""
+    arr = (ctypes.c_void_p * len(srcs))(*srcs)
+    return _L.ishmemi_c_combine(OPS[op], DTYPES[dtype], dst, arr, len(srcs), n, stream or None)
+
+
+def _make_blocking(op: str, dt: str):
+    def fn(*args):
+        # Overloads of the reference: (dest, source, nreduce) and (team, dest, source, nreduce).
+        if len(args) == 3:
+            team, (dest, source, n) = ISHMEM_TEAM_WORLD, args
+        elif len(args) == 4:
+            team, dest, source, n = args
+        else:
+            raise TypeError("expected ([team,] dest, source, nreduce)")
+        return _L.ishmemi_c_reduce(team, OPS[op], DTYPES[dt], dest, source, n)
+    return fn
+
+
+def _make_on_stream(op: str, dt: str):
+    def fn(*args):
+        if len(args) == 5:
+            team, (dest, source, n, ret, stream) = ISHMEM_TEAM_WORLD, args
+        elif len(args) == 6:
+            team, dest, source, n, ret, stream = args
+        else:
+            raise TypeError("expected ([team,] dest, source, nreduce, ret, stream)")
+        return _L.ishmemi_c_reduce_on_stream(team, OPS[op], DTYPES[dt], dest, source, n,
+                                             ret or None, stream or None)
+    return fn
+
+
+_mod = sys.modules[__name__]
+API_NAMES: list[str] = []
+for _op, _tns in TYPENAMES_FOR_OP.items():
+    for _tn in _tns:
+        _name = f"ishmem_{_tn}_{_op}_reduce"
+        _f = _make_blocking(_op, TYPENAMES[_tn])
+        _f.__name__ = _name
+        _f.__doc__ = f"{_name}([team,] dest, source, nreduce) -> int  (src/ishmem.h reduce section)"
+        setattr(_mod, _name, _f)
+        _xname = f"ishmemx_{_tn}_{_op}_reduce_on_stream"
+        _g = _make_on_stream(_op, TYPENAMES[_tn])
+        _g.__name__ = _xname
+        setattr(_mod, _xname, _g)
+        API_NAMES += [_name, _xname]
+del _op, _tns, _tn, _name, _f, _xname, _g

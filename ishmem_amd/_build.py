@@ -1,0 +1,73 @@
+"""Build the native library in-tree: ishmem_amd/libishmem_amd.so (HIP, gfx950).
+
+Plain hipcc invocations (no cmake / torch JIT) so the .so lives in the repo tree and travels to
+the GPU box with the snapshot.  Rebuilds only when a source or header is newer than the output.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+INCLUDE = ROOT / "include"
+BUILD = ROOT / "build" / "native"
+LIB = PKG / "libishmem_amd.so"
+
+SOURCES = ["kernels.hip", "runtime.cpp", "bootstrap.cpp"]
+ARCH = os.environ.get("ISHMEM_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: the ishmem_amd native library needs ROCm's hipcc")
+
+
+def _deps() -> list[Path]:
+    return sorted(list(CSRC.glob("*")) + list(INCLUDE.glob("*.h")))
+
+
+def needs_build() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in _deps())
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if not force and not needs_build():
+        return LIB
+    hipcc = _hipcc()
+    BUILD.mkdir(parents=True, exist_ok=True)
+    common = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
+              "-Wall", "-Wno-unused-function"]
+    objs = []
+    procs = []
+    for src in SOURCES:
+        obj = BUILD / (Path(src).stem + ".o")
+        objs.append(obj)
+        cmd = [hipcc, *common, "-c", str(CSRC / src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+    for cmd, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError(f"hipcc failed: {' '.join(cmd)}\n{out.decode(errors='replace')}")
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout.decode(errors='replace')}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

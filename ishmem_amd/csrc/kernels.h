@@ -1,0 +1,60 @@
+// ishmem_amd — kernel launch interface (host side of the HIP kernels in kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "types.h"
+
+namespace ishmemi {
+
+// One node of MI355X has 8 GPUs; 16 leaves room for several PEs per GPU (tests run 2-4 PEs
+// on one device).  The reference caps node-local PEs at 64 (src/ishmem/util.h:29).
+constexpr int kMaxPes = 16;
+// Upper bound of workgroups per collective launch; flag arrays are sized from it.
+constexpr int kMaxBlocks = 1024;
+// Barrier phases of one collective (start, mid, end) + a standalone team-sync phase.
+constexpr int kPhases = 4;
+constexpr int kPhaseStart = 0, kPhaseMid = 1, kPhaseEnd = 2, kPhaseSync = 3;
+// Per-team flag block: [phase][block][pe] uint32 epochs, then an error word.
+constexpr size_t kFlagWordsPerTeam = (size_t) kPhases * kMaxBlocks * kMaxPes;
+constexpr size_t kTeamFlagBytes = kFlagWordsPerTeam * 4 + 256;
+constexpr int kBlock = 256;  // 4 waves of 64
+constexpr int kUnroll = 4;   // items in flight per thread per source
+
+// Arguments of the multi-PE reduce-scatter + all-gather kernel.  All pointers are already
+// translated into this process's address space (own heap or IPC-mapped peer heap).
+struct ReduceArgs {
+    const char *src[kMaxPes];   // member j's source (element 0), j in team order
+    const char *dstp[kMaxPes];  // member j's dest (element 0), for all-gather pulls
+    char *dst;                  // own dest (element 0)
+    uint32_t *my_flags;         // own team flag block (fine-grained, written by peers)
+    uint32_t *peer_flags[kMaxPes];
+    uint32_t *err;  // own error word
+    int *ret;       // optional user status word (ishmemx_*_on_stream), may be null
+    uint64_t head;  // scalar elements before the 16-B aligned body (vector mode)
+    uint64_t nitems;  // body items (16-B vectors in vector mode, elements in scalar mode)
+    uint64_t tail;    // scalar elements after the body
+    uint64_t items_per_chunk;
+    uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
+    uint32_t epoch;
+    int p, me;
+};
+
+// Arguments of the local k-input fan-in combine: dst = op(src0, src1, ..., src_{k-1}).
+constexpr int kMaxFanin = 16;
+struct FaninArgs {
+    const char *src[kMaxFanin];
+    char *dst;
+    uint64_t head, nitems, tail;
+    int nsrc;
+};
+
+// Returns hipSuccess or a launch error.  `vec` selects the 16-B vector body (all operands
+// share the same address residue mod 16) or the element-granular path.
+hipError_t launch_allreduce(int op, int dt, bool vec, const ReduceArgs &a, int grid,
+                            hipStream_t s);
+hipError_t launch_fanin(int op, int dt, bool vec, const FaninArgs &a, int grid, hipStream_t s);
+hipError_t launch_team_sync(const ReduceArgs &a, hipStream_t s);
+
+}  // namespace ishmemi

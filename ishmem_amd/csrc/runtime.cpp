@@ -1,0 +1,840 @@
+// ishmem_amd — host runtime + C-ABI of the reduction-collective path.
+//
+// Reference layers replaced here: L1 device/memory substrate (Level-Zero
+// accelerator src/accelerator.cpp, symmetric heap src/memory.cpp:35-132, IPC handle exchange
+// src/ipc.cpp:123-233, team tables src/teams.cpp:73-161), and L4's host dispatch
+// ishmemi_reduce (src/collectives/reduce_impl.h:259-317) plus the on_queue launcher (:444-474).
+// The device data plane is in kernels.hip.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/prctl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <string>
+
+#include "bootstrap.h"
+#include "kernels.h"
+#include "types.h"
+
+namespace ishmemi {
+namespace {
+
+constexpr int kMaxTeams = 16;
+constexpr size_t kHeapAlign = 256;
+
+thread_local std::string g_last_error;
+
+int fail(const std::string &msg)
+{
+    g_last_error = msg;
+    if (getenv("ISHMEM_DEBUG") && atoi(getenv("ISHMEM_DEBUG")) > 0)
+        fprintf(stderr, "[ishmem_amd] %s\n", msg.c_str());
+    return 1;
+}
+
+int hipfail(const char *what, hipError_t e)
+{
+    return fail(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) return hipfail(#expr, e_);                                           \
+    } while (0)
+
+size_t parse_size(const char *s, size_t dflt)
+{
+    if (!s || !*s) return dflt;
+    char *end = nullptr;
+    double v = strtod(s, &end);
+    if (end && *end) {
+        switch (*end) {
+            case 'k': case 'K': v *= 1024.0; break;
+            case 'm': case 'M': v *= 1024.0 * 1024.0; break;
+            case 'g': case 'G': v *= 1024.0 * 1024.0 * 1024.0; break;
+            default: break;
+        }
+    }
+    return v > 0 ? (size_t) v : dflt;
+}
+
+long long env_ll(const char *name, long long dflt)
+{
+    const char *s = getenv(name);
+    return (s && *s) ? atoll(s) : dflt;
+}
+
+struct Team {
+    bool valid = false;
+    int start = 0, stride = 1, size = 1;  // in world PEs (src/teams.h:56-76)
+    int my_idx = -1;                      // my index in the team, -1 if not a member
+    uint32_t epoch = 0;                   // last epoch used by a collective of this team
+};
+
+struct PeRecord {
+    int32_t pe, pid, device, flags_fine_grained;
+    uint64_t heap_size;
+    hipIpcMemHandle_t heap_handle;
+    hipIpcMemHandle_t flags_handle;
+};
+
+struct State {
+    std::mutex mu;
+    bool initialized = false;
+    int pe = 0, npes = 1, device = 0;
+    ShmBootstrap boot;
+
+    char *heap = nullptr;
+    size_t heap_size = 0;
+    std::map<size_t, size_t> free_list;  // offset -> bytes
+    std::map<size_t, size_t> used;       // offset -> bytes
+    char *peer_heap[kMaxPes] = {};
+
+    uint32_t *flags = nullptr;  // kMaxTeams flag blocks, fine-grained device memory
+    bool flags_fine_grained = false;
+    uint32_t *peer_flags[kMaxPes] = {};
+    uint32_t *err_host = nullptr;  // host-mapped error words, one per team
+    uint32_t *err_dev = nullptr;
+
+    char *staging = nullptr;  // symmetric staging region for non-heap / host buffers
+    size_t staging_bytes = 0;
+
+    Team teams[kMaxTeams];
+    int max_blocks = kMaxBlocks;
+    long long timeout_ms = 60000;
+    int debug = 0;
+    int error_count = 0;
+};
+
+State &S()
+{
+    static State s;
+    return s;
+}
+
+bool in_heap(const State &s, const void *p)
+{
+    return s.heap && (const char *) p >= s.heap && (const char *) p < s.heap + s.heap_size;
+}
+
+// Address of heap pointer `p` (own heap) as mapped in this process for world PE `pe`.
+char *translate(const State &s, const void *p, int pe)
+{
+    if (!in_heap(s, p)) return nullptr;
+    if (pe == s.pe) return (char *) p;
+    if (pe < 0 || pe >= s.npes || !s.peer_heap[pe]) return nullptr;
+    return s.peer_heap[pe] + ((const char *) p - s.heap);
+}
+
+uint32_t *team_flags(uint32_t *base, int team)
+{
+    return base ? base + (size_t) team * (kTeamFlagBytes / 4) : nullptr;
+}
+
+// ---------------- symmetric heap allocator (deterministic first fit, same on every PE) -------
+void *heap_alloc(State &s, size_t bytes, size_t align)
+{
+    if (bytes == 0) bytes = 1;
+    align = std::max(align, kHeapAlign);
+    bytes = (bytes + kHeapAlign - 1) & ~(kHeapAlign - 1);
+    for (auto it = s.free_list.begin(); it != s.free_list.end(); ++it) {
+        const size_t off = it->first, len = it->second;
+        const size_t aligned = (off + align - 1) & ~(align - 1);
+        if (aligned + bytes > off + len) continue;
+        s.free_list.erase(it);
+        if (aligned > off) s.free_list[off] = aligned - off;
+        if (aligned + bytes < off + len) s.free_list[aligned + bytes] = off + len - aligned - bytes;
+        s.used[aligned] = bytes;
+        return s.heap + aligned;
+    }
+    fail("ishmem_malloc: symmetric heap exhausted (raise ISHMEM_SYMMETRIC_SIZE)");
+    return nullptr;
+}
+
+void heap_free(State &s, void *p)
+{
+    if (!p || !in_heap(s, p)) return;
+    const size_t off = (char *) p - s.heap;
+    auto it = s.used.find(off);
+    if (it == s.used.end()) return;
+    size_t start = off, len = it->second;
+    s.used.erase(it);
+    auto next = s.free_list.lower_bound(start);
+    if (next != s.free_list.end() && next->first == start + len) {
+        len += next->second;
+        s.free_list.erase(next);
+    }
+    auto prev = s.free_list.lower_bound(start);
+    if (prev != s.free_list.begin()) {
+        --prev;
+        if (prev->first + prev->second == start) {
+            start = prev->first;
+            len += prev->second;
+            s.free_list.erase(prev);
+        }
+    }
+    s.free_list[start] = len;
+}
+
+// ---------------- launch planning ----------------------------------------------------------
+struct Plan {
+    bool vec;
+    uint64_t head, nitems, tail, items_per_chunk;
+    int grid;
+};
+
+// The partition of the multi-PE schedule: member c owns items [c*ipc, min((c+1)*ipc, n)),
+// ipc rounded up to 64 items (1 KiB of 16-B vectors) so chunk edges stay line aligned.
+uint64_t items_per_chunk(uint64_t nitems, int npes)
+{
+    const uint64_t per = (nitems + (uint64_t) npes - 1) / (uint64_t) npes;
+    return std::max<uint64_t>(64, (per + 63) & ~uint64_t(63));
+}
+
+Plan make_plan(const void *dst, const void *const *srcs, int nsrc, size_t n, size_t es, int npes,
+               int max_blocks, int max_grid)
+{
+    Plan pl{};
+    const uintptr_t d = (uintptr_t) dst;
+    bool same_residue = (d % es) == 0;
+    for (int i = 0; i < nsrc; ++i) {
+        const uintptr_t sp = (uintptr_t) srcs[i];
+        same_residue = same_residue && ((sp ^ d) & 15) == 0 && (sp % es) == 0;
+    }
+    pl.vec = same_residue;
+    if (pl.vec) {
+        const size_t mis = d & 15;
+        pl.head = std::min<uint64_t>(n, mis ? (16 - mis) / es : 0);
+        const uint64_t ve = 16 / es;
+        pl.nitems = (n - pl.head) / ve;
+        pl.tail = n - pl.head - pl.nitems * ve;
+    } else {
+        pl.head = 0;
+        pl.nitems = n;
+        pl.tail = 0;
+    }
+    const uint64_t tile = (uint64_t) kBlock * kUnroll;
+    if (npes > 1) {
+        pl.items_per_chunk = items_per_chunk(pl.nitems, npes);
+        const uint64_t g = (pl.items_per_chunk + tile - 1) / tile;
+        pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t) max_blocks));
+    } else {
+        pl.items_per_chunk = pl.nitems;
+        const uint64_t g = (pl.nitems + tile - 1) / tile;
+        pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t) max_grid));
+    }
+    return pl;
+}
+
+// Fills the kernel arguments common to every collective of `team`.
+int team_args(State &s, int team, ReduceArgs &a, std::string &why)
+{
+    Team &t = s.teams[team];
+    memset(&a, 0, sizeof(a));
+    a.p = t.size;
+    a.me = t.my_idx;
+    a.my_flags = team_flags(s.flags, team);
+    a.err = s.err_dev + team;
+    a.timeout_ticks = (uint64_t) s.timeout_ms * 100000ull;  // s_memrealtime runs at 100 MHz
+    for (int j = 0; j < t.size; ++j) {
+        const int gpe = t.start + j * t.stride;
+        a.peer_flags[j] = team_flags(s.peer_flags[gpe], team);
+        if (!a.peer_flags[j]) {
+            why = "team member " + std::to_string(gpe) + " has no mapped flag block";
+            return 1;
+        }
+    }
+    if (++t.epoch == 0) t.epoch = 1;
+    a.epoch = t.epoch;
+    return 0;
+}
+
+int check_team_errors(State &s, int team)
+{
+    const uint32_t e = __atomic_load_n(&s.err_host[team], __ATOMIC_ACQUIRE);
+    if (e) {
+        __atomic_store_n(&s.err_host[team], 0u, __ATOMIC_RELEASE);
+        s.error_count++;
+        return fail("device barrier timed out (phase mask 0x" + std::to_string(e) +
+                    "): a team member did not arrive within timeout_ms");
+    }
+    return 0;
+}
+
+enum class Kind { Heap, Device, Host };
+
+Kind classify(const State &s, const void *p)
+{
+    if (in_heap(s, p)) return Kind::Heap;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) == hipSuccess) {
+        if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) return Kind::Device;
+        return Kind::Host;
+    }
+    (void) hipGetLastError();
+    return Kind::Host;
+}
+
+int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)
+{
+    if (bytes == 0 || dst == src) return 0;
+    FaninArgs f{};
+    f.src[0] = (const char *) src;
+    f.dst = (char *) dst;
+    f.nsrc = 1;
+    const void *srcs[1] = {src};
+    Plan pl = make_plan(dst, srcs, 1, bytes, 1, 1, 0, 2048);
+    f.head = pl.head;
+    f.nitems = pl.nitems;
+    f.tail = pl.tail;
+    HIP_TRY(launch_fanin(ISHMEMI_OP_OR, ISHMEMI_DT_UINT8, pl.vec, f, pl.grid, st));
+    return 0;
+}
+
+// Device-resident collective on symmetric-heap buffers: one allreduce_kernel launch.
+int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, size_t n, int *ret,
+                hipStream_t st)
+{
+    Team &t = s.teams[team];
+    const size_t es = dtype_size(dt);
+    ReduceArgs a;
+    std::string why;
+    if (team_args(s, team, a, why)) return fail("reduce: " + why);
+    for (int j = 0; j < t.size; ++j) {
+        const int gpe = t.start + j * t.stride;
+        a.src[j] = translate(s, src, gpe);
+        a.dstp[j] = translate(s, dst, gpe);
+        if (!a.src[j] || !a.dstp[j])
+            return fail("reduce: buffer not mapped for PE " + std::to_string(gpe));
+    }
+    a.dst = (char *) dst;
+    a.ret = ret;
+    const void *srcs[1] = {src};
+    Plan pl = make_plan(dst, srcs, 1, n, es, t.size, s.max_blocks, 0);
+    a.head = pl.head;
+    a.nitems = pl.nitems;
+    a.tail = pl.tail;
+    a.items_per_chunk = pl.items_per_chunk;
+    HIP_TRY(launch_allreduce(op, dt, pl.vec, a, pl.grid, st));
+    return 0;
+}
+
+int team_sync_locked(State &s, int team, hipStream_t st, int *ret)
+{
+    Team &t = s.teams[team];
+    if (t.size <= 1) return 0;
+    ReduceArgs a;
+    std::string why;
+    if (team_args(s, team, a, why)) return fail("team_sync: " + why);
+    a.ret = ret;
+    HIP_TRY(launch_team_sync(a, st));
+    return 0;
+}
+
+int reduce_impl(int team, int op, int dt, void *dst, const void *src, size_t n, int *ret,
+                hipStream_t st, bool blocking)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.initialized) return fail("reduce: ishmem not initialized");
+    if (!op_dtype_valid(op, dt)) return fail("reduce: invalid (op, dtype) pair");
+    if (team < 0 || team >= kMaxTeams || !s.teams[team].valid)
+        return fail("reduce: invalid team handle");
+    Team &t = s.teams[team];
+    if (t.my_idx < 0) return fail("reduce: calling PE is not a member of the team");
+    if (n > 0 && (!dst || !src)) return fail("reduce: null buffer");
+    const size_t es = dtype_size(dt);
+    const size_t bytes = n * es;
+
+    if (t.size == 1) {
+        // One PE: the reduction is a copy (reduce_impl.h:288-289 with no peers to fold).
+        if (n > 0 && dst != src) {
+            const Kind kd = classify(s, dst), ks = classify(s, src);
+            if (kd == Kind::Host || ks == Kind::Host) {
+                HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
+            } else if (launch_copy(dst, src, bytes, st)) {
+                return 1;
+            }
+        }
+        if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
+    } else if (n == 0) {
+        // The reference still synchronises the team (reduce_impl.h:244, :254).
+        if (team_sync_locked(s, team, st, ret)) return 1;
+    } else if (in_heap(s, dst) && in_heap(s, src)) {
+        if (reduce_heap(s, team, op, dt, dst, src, n, ret, st)) return 1;
+    } else {
+        // Non-symmetric buffers (host memory, or device memory outside the heap): stage each
+        // chunk through the symmetric staging region, reduce it in place there, copy it out.
+        // Replaces the 64 KiB host bounce loop ishmemi_generic_op_reduce (reduce_impl.h:186-228).
+        const size_t chunk = (s.staging_bytes / es) & ~size_t(63);
+        if (chunk == 0) return fail("reduce: staging region too small");
+        for (size_t off = 0; off < n; off += chunk) {
+            const size_t m = std::min(chunk, n - off);
+            HIP_TRY(hipMemcpyAsync(s.staging, (const char *) src + off * es, m * es,
+                                   hipMemcpyDefault, st));
+            if (reduce_heap(s, team, op, dt, s.staging, s.staging, m, ret, st)) return 1;
+            HIP_TRY(hipMemcpyAsync((char *) dst + off * es, s.staging, m * es, hipMemcpyDefault,
+                                   st));
+        }
+    }
+    if (blocking) {
+        HIP_TRY(hipStreamSynchronize(st));
+        if (check_team_errors(s, team)) return 1;
+    }
+    return 0;
+}
+
+int init_impl(int pe, int npes, int device, const std::string &key)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (s.initialized) return 0;
+    if (npes < 1 || npes > kMaxPes || pe < 0 || pe >= npes)
+        return fail("init: invalid pe/npes (npes must be 1.." + std::to_string(kMaxPes) + ")");
+    s.pe = pe;
+    s.npes = npes;
+    s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, env_ll("ISHMEM_MAX_BLOCKS", kMaxBlocks)));
+    s.timeout_ms = std::max<long long>(1, env_ll("ISHMEM_TIMEOUT_MS", 60000));
+    s.debug = (int) env_ll("ISHMEM_DEBUG", 0);
+
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (ndev < 1) return fail("init: no HIP device visible");
+    s.device = device >= 0 ? device % ndev : 0;
+    HIP_TRY(hipSetDevice(s.device));
+
+    // Symmetric heap: ONE hipMalloc (coarse-grained HBM) per PE, src/memory.cpp:35-132.
+    s.heap_size = parse_size(getenv("ISHMEM_SYMMETRIC_SIZE"), (size_t) 4 << 30);
+    s.heap_size = (s.heap_size + (2u << 20) - 1) & ~(size_t) ((2u << 20) - 1);
+    HIP_TRY(hipMalloc((void **) &s.heap, s.heap_size));
+    s.free_list.clear();
+    s.used.clear();
+    s.free_list[0] = s.heap_size;
+
+    // Barrier flags: fine-grained (uncached) device memory, written by peers over xGMI.
+    const size_t flag_bytes = (size_t) kMaxTeams * kTeamFlagBytes;
+    if (hipExtMallocWithFlags((void **) &s.flags, flag_bytes, hipDeviceMallocUncached) == hipSuccess) {
+        s.flags_fine_grained = true;
+    } else {
+        (void) hipGetLastError();
+        HIP_TRY(hipMalloc((void **) &s.flags, flag_bytes));
+        s.flags_fine_grained = false;
+    }
+    HIP_TRY(hipMemset(s.flags, 0, flag_bytes));
+    HIP_TRY(hipHostMalloc((void **) &s.err_host, kMaxTeams * sizeof(uint32_t),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    memset(s.err_host, 0, kMaxTeams * sizeof(uint32_t));
+    HIP_TRY(hipHostGetDevicePointer((void **) &s.err_dev, s.err_host, 0));
+    HIP_TRY(hipDeviceSynchronize());
+
+    for (int i = 0; i < kMaxPes; ++i) {
+        s.peer_heap[i] = nullptr;
+        s.peer_flags[i] = nullptr;
+    }
+    s.peer_heap[pe] = s.heap;
+    s.peer_flags[pe] = s.flags;
+
+    if (npes > 1) {
+        // Let peers import our dma-buf handles (pidfd_getfd needs ptrace rights under Yama).
+        prctl(PR_SET_PTRACER, PR_SET_PTRACER_ANY, 0, 0, 0);
+        std::string err;
+        if (s.boot.attach(pe, npes, key, (int) std::max<long long>(s.timeout_ms, 10000), err))
+            return fail(err);
+        PeRecord mine{};
+        mine.pe = pe;
+        mine.pid = (int32_t) getpid();
+        mine.device = s.device;
+        mine.flags_fine_grained = s.flags_fine_grained ? 1 : 0;
+        mine.heap_size = s.heap_size;
+        HIP_TRY(hipIpcGetMemHandle(&mine.heap_handle, s.heap));
+        if (hipIpcGetMemHandle(&mine.flags_handle, s.flags) != hipSuccess) {
+            // Uncached allocations that cannot be exported: fall back to coarse-grained flags
+            // (every flag access is a system-scope atomic, so correctness does not depend on it).
+            (void) hipGetLastError();
+            hipFree(s.flags);
+            HIP_TRY(hipMalloc((void **) &s.flags, flag_bytes));
+            HIP_TRY(hipMemset(s.flags, 0, flag_bytes));
+            HIP_TRY(hipDeviceSynchronize());
+            s.flags_fine_grained = false;
+            s.peer_flags[pe] = s.flags;
+            mine.flags_fine_grained = 0;
+            HIP_TRY(hipIpcGetMemHandle(&mine.flags_handle, s.flags));
+        }
+        PeRecord all[kMaxPes];
+        if (s.boot.allgather(&mine, all, sizeof(PeRecord), err)) return fail(err);
+        for (int j = 0; j < npes; ++j) {
+            if (j == pe) continue;
+            if (all[j].heap_size != s.heap_size)
+                return fail("init: ISHMEM_SYMMETRIC_SIZE differs between PEs");
+            if (all[j].device != s.device) {
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, s.device, all[j].device) == hipSuccess && can) {
+                    hipError_t e = hipDeviceEnablePeerAccess(all[j].device, 0);
+                    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                        return hipfail("hipDeviceEnablePeerAccess", e);
+                    (void) hipGetLastError();
+                }
+            }
+            HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_heap[j], all[j].heap_handle,
+                                        hipIpcMemLazyEnablePeerAccess));
+            HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_flags[j], all[j].flags_handle,
+                                        hipIpcMemLazyEnablePeerAccess));
+        }
+        if (s.boot.barrier(err)) return fail(err);
+    }
+
+    // Teams: WORLD, SHARED, NODE all span the node (src/teams.cpp:108-257).
+    for (int i = 0; i < kMaxTeams; ++i) s.teams[i] = Team{};
+    for (int i = 0; i <= ISHMEMI_C_TEAM_NODE; ++i) {
+        Team &t = s.teams[i];
+        t.valid = true;
+        t.start = 0;
+        t.stride = 1;
+        t.size = npes;
+        t.my_idx = pe;
+    }
+    // Symmetric staging region (first allocation on every PE, hence the same offset).
+    s.staging_bytes = parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 64 << 20);
+    s.staging = (char *) heap_alloc(s, s.staging_bytes, kHeapAlign);
+    if (!s.staging) return 1;
+    s.initialized = true;
+    return 0;
+}
+
+std::string default_key()
+{
+    if (const char *k = getenv("ISHMEM_BOOTSTRAP_KEY")) return k;
+    std::string key = "job";
+    if (const char *p = getenv("MASTER_PORT")) key += std::string("_p") + p;
+    if (const char *r = getenv("TORCHELASTIC_RUN_ID")) key += std::string("_") + r;
+    return key;
+}
+
+int env_int(const char *a, const char *b, int dflt)
+{
+    if (const char *s = getenv(a)) return atoi(s);
+    if (b)
+        if (const char *s = getenv(b)) return atoi(s);
+    return dflt;
+}
+
+}  // namespace
+}  // namespace ishmemi
+
+using namespace ishmemi;
+
+extern "C" {
+
+int ishmemi_c_init(void)
+{
+    const int pe = env_int("ISHMEM_PE", "RANK", 0);
+    const int npes = env_int("ISHMEM_NPES", "WORLD_SIZE", 1);
+    const int dev = env_int("ISHMEM_DEVICE", "LOCAL_RANK", 0);
+    return init_impl(pe, npes, dev, default_key());
+}
+
+int ishmemi_c_init_pe(int pe, int npes, int device, const char *key)
+{
+    if (device < 0) device = env_int("ISHMEM_DEVICE", "LOCAL_RANK", 0);
+    return init_impl(pe, npes, device, key && *key ? std::string(key) : default_key());
+}
+
+int ishmemi_c_finalize(void)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.initialized) return 0;
+    hipDeviceSynchronize();
+    if (s.npes > 1) {
+        std::string err;
+        s.boot.barrier(err);  // no peer may still be reading our heap
+        for (int j = 0; j < s.npes; ++j) {
+            if (j == s.pe) continue;
+            if (s.peer_heap[j]) hipIpcCloseMemHandle(s.peer_heap[j]);
+            if (s.peer_flags[j]) hipIpcCloseMemHandle(s.peer_flags[j]);
+            s.peer_heap[j] = nullptr;
+            s.peer_flags[j] = nullptr;
+        }
+        s.boot.barrier(err);
+        s.boot.detach();
+    }
+    hipFree(s.heap);
+    hipFree(s.flags);
+    hipHostFree(s.err_host);
+    s.heap = nullptr;
+    s.flags = nullptr;
+    s.err_host = s.err_dev = nullptr;
+    s.initialized = false;
+    return 0;
+}
+
+int ishmemi_c_initialized(void) { return S().initialized ? 1 : 0; }
+int ishmemi_c_my_pe(void) { return S().initialized ? S().pe : -1; }
+int ishmemi_c_n_pes(void) { return S().initialized ? S().npes : -1; }
+int ishmemi_c_device(void) { return S().initialized ? S().device : -1; }
+
+void *ishmemi_c_align(size_t alignment, size_t size)
+{
+    State &s = S();
+    void *p;
+    {
+        std::lock_guard<std::mutex> lk(s.mu);
+        if (!s.initialized) {
+            fail("ishmem_malloc: not initialized");
+            return nullptr;
+        }
+        if (alignment & (alignment - 1)) {
+            fail("ishmem_align: alignment must be a power of two");
+            return nullptr;
+        }
+        p = heap_alloc(s, size, alignment ? alignment : kHeapAlign);
+    }
+    // Collective like the reference (barrier on every alloc, src/memory.cpp:234).
+    if (s.npes > 1) {
+        std::string err;
+        if (s.boot.barrier(err)) fail(err);
+    }
+    return p;
+}
+
+void *ishmemi_c_malloc(size_t size) { return ishmemi_c_align(kHeapAlign, size); }
+
+void *ishmemi_c_calloc(size_t count, size_t size)
+{
+    void *p = ishmemi_c_align(kHeapAlign, count * size);
+    if (p && hipMemset(p, 0, count * size) != hipSuccess) {
+        fail("ishmem_calloc: hipMemset failed");
+        return nullptr;
+    }
+    return p;
+}
+
+void ishmemi_c_free(void *ptr)
+{
+    State &s = S();
+    if (!s.initialized) return;
+    hipDeviceSynchronize();
+    if (s.npes > 1) {  // src/memory.cpp:286: peers must be done with the buffer
+        std::string err;
+        s.boot.barrier(err);
+    }
+    std::lock_guard<std::mutex> lk(s.mu);
+    heap_free(s, ptr);
+}
+
+void *ishmemi_c_ptr(const void *dest, int pe)
+{
+    State &s = S();
+    if (!s.initialized) return nullptr;
+    return translate(s, dest, pe);
+}
+
+int ishmemi_c_heap_info(void **base, size_t *size, size_t *used)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (base) *base = s.heap;
+    if (size) *size = s.heap_size;
+    if (used) {
+        size_t u = 0;
+        for (auto &kv : s.used) u += kv.second;
+        *used = u;
+    }
+    return s.initialized ? 0 : 1;
+}
+
+int ishmemi_c_team_my_pe(int team)
+{
+    State &s = S();
+    if (!s.initialized || team < 0 || team >= kMaxTeams || !s.teams[team].valid) return -1;
+    return s.teams[team].my_idx;
+}
+
+int ishmemi_c_team_n_pes(int team)
+{
+    State &s = S();
+    if (!s.initialized || team < 0 || team >= kMaxTeams || !s.teams[team].valid) return -1;
+    return s.teams[team].size;
+}
+
+int ishmemi_c_team_translate_pe(int src_team, int src_pe, int dest_team)
+{
+    State &s = S();
+    if (!s.initialized) return -1;
+    if (src_team < 0 || src_team >= kMaxTeams || dest_team < 0 || dest_team >= kMaxTeams) return -1;
+    const Team &a = s.teams[src_team], &b = s.teams[dest_team];
+    if (!a.valid || !b.valid || src_pe < 0 || src_pe >= a.size) return -1;
+    const int gpe = a.start + src_pe * a.stride;
+    if (b.stride == 0) return -1;
+    const int d = gpe - b.start;
+    if (d % b.stride) return -1;
+    const int idx = d / b.stride;
+    return (idx >= 0 && idx < b.size) ? idx : -1;
+}
+
+int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, int *new_team)
+{
+    State &s = S();
+    if (new_team) *new_team = ISHMEMI_C_TEAM_INVALID;
+    int slot = -1;
+    {
+        std::lock_guard<std::mutex> lk(s.mu);
+        if (!s.initialized) return fail("team_split_strided: not initialized");
+        if (parent < 0 || parent >= kMaxTeams || !s.teams[parent].valid)
+            return fail("team_split_strided: invalid parent team");
+        const Team &pt = s.teams[parent];
+        if (pt.my_idx < 0) return fail("team_split_strided: caller not in parent team");
+        if (size < 1 || start < 0 || start >= pt.size || (size > 1 && stride < 1) ||
+            start + (size - 1) * std::max(stride, 0) >= pt.size)
+            return fail("team_split_strided: invalid triplet");
+        for (int i = ISHMEMI_C_TEAM_NODE + 1; i < kMaxTeams; ++i)
+            if (!s.teams[i].valid) {
+                slot = i;
+                break;
+            }
+        if (slot < 0) return fail("team_split_strided: no free team slot");
+        Team t;
+        t.valid = true;
+        t.start = pt.start + start * pt.stride;
+        t.stride = (size > 1 ? stride : 1) * pt.stride;
+        t.size = size;
+        const int d = s.pe - t.start;
+        t.my_idx = (d >= 0 && d % t.stride == 0 && d / t.stride < size) ? d / t.stride : -1;
+        t.epoch = 0;
+        s.teams[slot] = t;
+        // Fresh flag block: zero it locally, then the parent sync below orders the zeroing
+        // before any member's first barrier on the new team.
+        if (hipMemset(team_flags(s.flags, slot), 0, kTeamFlagBytes) != hipSuccess)
+            return fail("team_split_strided: flag reset failed");
+        if (hipDeviceSynchronize() != hipSuccess) return fail("team_split_strided: sync failed");
+    }
+    if (ishmemi_c_team_sync(parent)) return 1;
+    if (new_team && s.teams[slot].my_idx >= 0) *new_team = slot;
+    return 0;
+}
+
+void ishmemi_c_team_destroy(int team)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (team <= ISHMEMI_C_TEAM_NODE || team >= kMaxTeams) return;
+    s.teams[team] = Team{};
+}
+
+int ishmemi_c_team_sync(int team)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.initialized) return fail("team_sync: not initialized");
+    if (team < 0 || team >= kMaxTeams || !s.teams[team].valid) return fail("team_sync: invalid team");
+    if (s.teams[team].my_idx < 0) return fail("team_sync: caller not in team");
+    if (team_sync_locked(s, team, 0, nullptr)) return 1;
+    HIP_TRY(hipStreamSynchronize(0));
+    return check_team_errors(s, team);
+}
+
+int ishmemi_c_sync_all(void) { return ishmemi_c_team_sync(ISHMEMI_C_TEAM_WORLD); }
+
+int ishmemi_c_barrier_all(void)
+{
+    // ishmem_barrier_all = quiet + sync_all: complete all outstanding device work first.
+    if (hipDeviceSynchronize() != hipSuccess) return fail("barrier_all: device sync failed");
+    return ishmemi_c_team_sync(ISHMEMI_C_TEAM_WORLD);
+}
+
+int ishmemi_c_reduce(int team, int op, int dtype, void *dest, const void *source, size_t nreduce)
+{
+    return reduce_impl(team, op, dtype, dest, source, nreduce, nullptr, 0, true);
+}
+
+int ishmemi_c_reduce_on_stream(int team, int op, int dtype, void *dest, const void *source,
+                               size_t nreduce, int *ret, void *stream)
+{
+    return reduce_impl(team, op, dtype, dest, source, nreduce, ret, (hipStream_t) stream, false);
+}
+
+int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n,
+                      void *stream)
+{
+    if (!op_dtype_valid(op, dtype)) return fail("combine: invalid (op, dtype) pair");
+    if (nsrc < 1 || nsrc > kMaxFanin) return fail("combine: nsrc must be 1..16");
+    if (n == 0) return 0;
+    if (!dst || !srcs) return fail("combine: null pointer");
+    FaninArgs f{};
+    for (int i = 0; i < nsrc; ++i) {
+        if (!srcs[i]) return fail("combine: null source");
+        f.src[i] = (const char *) srcs[i];
+    }
+    f.dst = (char *) dst;
+    f.nsrc = nsrc;
+    Plan pl = make_plan(dst, srcs, nsrc, n, dtype_size(dtype), 1, 0, 2048);
+    f.head = pl.head;
+    f.nitems = pl.nitems;
+    f.tail = pl.tail;
+    HIP_TRY(launch_fanin(op, dtype, pl.vec, f, pl.grid, (hipStream_t) stream));
+    return 0;
+}
+
+const char *ishmemi_c_last_error(void) { return g_last_error.c_str(); }
+
+int ishmemi_c_set_param(const char *name, long long value)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    const std::string n = name ? name : "";
+    if (n == "max_blocks") s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, value));
+    else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
+    else if (n == "debug") s.debug = (int) value;
+    else return fail("set_param: unknown parameter " + n);
+    return 0;
+}
+
+long long ishmemi_c_get_param(const char *name)
+{
+    State &s = S();
+    const std::string n = name ? name : "";
+    if (n == "max_blocks") return s.max_blocks;
+    if (n == "timeout_ms") return s.timeout_ms;
+    if (n == "debug") return s.debug;
+    if (n == "flags_fine_grained") return s.flags_fine_grained ? 1 : 0;
+    if (n == "staging_bytes") return (long long) s.staging_bytes;
+    return -1;
+}
+
+int ishmemi_c_error_count(void) { return S().error_count; }
+
+size_t ishmemi_c_dtype_size(int dtype)
+{
+    return (dtype >= 0 && dtype < ISHMEMI_DT_COUNT) ? dtype_size(dtype) : 0;
+}
+
+int ishmemi_c_op_dtype_valid(int op, int dtype) { return op_dtype_valid(op, dtype) ? 1 : 0; }
+
+int ishmemi_c_chunk_bounds(uint64_t nitems, int npes, int c, uint64_t *begin, uint64_t *end)
+{
+    if (npes < 1 || c < 0 || c >= npes || !begin || !end) return 1;
+    const uint64_t ipc = npes > 1 ? items_per_chunk(nitems, npes) : nitems;
+    *begin = std::min<uint64_t>((uint64_t) c * ipc, nitems);
+    *end = std::min<uint64_t>(*begin + ipc, nitems);
+    return 0;
+}
+
+int ishmemi_c_bootstrap_selftest(int pe, int npes, const char *key, int value, int *out)
+{
+    ShmBootstrap b;
+    std::string err;
+    if (b.attach(pe, npes, key ? key : "selftest", 20000, err)) return fail(err);
+    if (b.allgather(&value, out, sizeof(int), err)) return fail(err);
+    if (b.barrier(err)) return fail(err);
+    return 0;
+}
+
+const char *ishmemi_c_version(void) { return "ishmem_amd 0.1.0 (reduction path; ref ishmem 1.5.1)"; }
+
+}  // extern "C"

@@ -1,0 +1,229 @@
+"""Worker body of the multi-PE GPU tests: one process = one PE, all PEs on one GPU, symmetric
+heaps mapped into each other over HIP IPC — the same code path as one PE per GPU over xGMI.
+
+Each worker regenerates every PE's inputs (deterministic seeds), runs the collective through
+the C-ABI and checks its own result against the ORACLE (tests only) and, where the inputs are
+the golden ones, against MPICH's MPI_Allreduce output in tests/golden.  Failures are returned
+as strings through the queue.
+"""
+from __future__ import annotations
+
+import os
+import traceback
+from pathlib import Path
+
+import numpy as np
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def _bits_equal(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8))
+
+
+def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None = None) -> None:
+    fails: list[str] = []
+    try:
+        for k, v in (env or {}).items():
+            os.environ[k] = str(v)
+        import oracle
+        import ishmem_amd as ish
+        from ishmem_amd import hip
+
+        ish.init(pe, npes, 0, key)
+        OPS, DT = oracle.OPS, oracle.DTYPES
+        NAMES = {v: k for k, v in DT.items()}
+        ONAMES = {v: k for k, v in OPS.items()}
+
+        def heap(n, dt):
+            return ish.ishmem_malloc(max(1, n * np.dtype(oracle.NP[dt]).itemsize))
+
+        def check(tag, op, dt, srcs, got, golden=None):
+            ref = oracle.reduce_fold(op, dt, srcs, 0)  # canonical team order = every PE's result
+            if not _bits_equal(got, ref):
+                bad = np.nonzero(got.view(np.uint8) != ref.view(np.uint8))[0]
+                fails.append(f"pe{pe} {tag}: {len(bad)} bytes differ from oracle (first byte {bad[:3]})")
+                return
+            if golden is not None:
+                if dt >= 8 and op in (OPS["sum"], OPS["prod"]):
+                    tol = oracle.fp_tolerance(dt, op, srcs, ref)
+                    if not np.all(np.abs(golden.astype(np.float64) - got.astype(np.float64)) <= tol):
+                        fails.append(f"pe{pe} {tag}: outside tolerance vs MPICH golden")
+                elif not _bits_equal(golden, got):
+                    fails.append(f"pe{pe} {tag}: differs from MPICH golden")
+
+        if "golden" in scenarios:
+            z = np.load(GOLDEN / f"golden_np{npes}.npz") if (GOLDEN / f"golden_np{npes}.npz").exists() else None
+            for op in range(7):
+                for dt in range(10):
+                    if not oracle.valid(op, dt):
+                        continue
+                    cases = []
+                    if z is not None:
+                        for nm in (f"rnd_{ONAMES[op]}_{NAMES[dt]}_1001", f"pat_{ONAMES[op]}_{NAMES[dt]}_129",
+                                   f"pat_{ONAMES[op]}_{NAMES[dt]}_3"):
+                            ins = list(z[nm + "__in"])
+                            outs = z[nm + "__out"]
+                            cases.append((nm, ins, outs[pe] if len(outs) > 1 else outs[0]))
+                    else:
+                        lo, hi = (0.5, 2.0) if op == OPS["prod"] else (-1.0, 1.0)
+                        ins = [oracle.fill_random(dt, 0x15AE0001 + j, 1001, lo, hi) for j in range(npes)]
+                        cases.append((f"rnd_{op}_{dt}", ins, None))
+                    for nm, ins, gold in cases:
+                        n = len(ins[0])
+                        s, d = heap(n, dt), heap(n, dt)
+                        hip.upload(s, ins[pe])
+                        r = ish.reduce(ONAMES[op], NAMES[dt], d, s, n)
+                        if r != 0:
+                            fails.append(f"pe{pe} {nm}: rc={r} {ish.last_error()}")
+                        else:
+                            check(nm, op, dt, ins, hip.download(d, n, oracle.NP[dt]), gold)
+                        ish.ishmem_free(d)
+                        ish.ishmem_free(s)
+
+        if "inplace" in scenarios:
+            for op, dt, n in [(OPS["sum"], DT["float"], 5000), (OPS["max"], DT["int64"], 777),
+                              (OPS["xor"], DT["uint8"], 100003), (OPS["prod"], DT["double"], 31)]:
+                lo, hi = (0.5, 2.0) if op == OPS["prod"] else (-1.0, 1.0)
+                ins = [oracle.fill_random(dt, 77 + j, n, lo, hi) for j in range(npes)]
+                b = heap(n, dt)
+                hip.upload(b, ins[pe])
+                r = ish.reduce(ONAMES[op], NAMES[dt], b, b, n)
+                if r:
+                    fails.append(f"pe{pe} inplace rc={r} {ish.last_error()}")
+                else:
+                    check(f"inplace {op} {dt} {n}", op, dt, ins, hip.download(b, n, oracle.NP[dt]))
+                ish.ishmem_free(b)
+
+        if "offsets" in scenarios:
+            # The reference tester's offset sweep (ishmem_tester.h:1407-1436): nelems 1..16 x
+            # src/dst byte offsets 0..14 step sizeof(T): exercises head/tail and scalar paths.
+            for dt in (DT["int8"], DT["int16"], DT["float"], DT["double"]):
+                es = np.dtype(oracle.NP[dt]).itemsize
+                base_s, base_d = heap(64, dt), heap(64, dt)
+                for nelems in (1, 2, 5, 16, 17, 40):
+                    for so in range(0, 15, es * 3):
+                        for do in range(0, 15, es * 5):
+                            op = OPS["sum"] if dt >= 8 else OPS["min"]
+                            ins = [oracle.fill_random(dt, 1000 + 7 * j + nelems, nelems) for j in range(npes)]
+                            hip.upload(base_s + so, ins[pe])
+                            r = ish.reduce(ONAMES[op], NAMES[dt], base_d + do, base_s + so, nelems)
+                            if r:
+                                fails.append(f"pe{pe} offsets rc={r} {ish.last_error()}")
+                                continue
+                            check(f"offsets dt{dt} n{nelems} so{so} do{do}", op, dt, ins,
+                                  hip.download(base_d + do, nelems, oracle.NP[dt]))
+                ish.ishmem_free(base_d)
+                ish.ishmem_free(base_s)
+
+        if "edge" in scenarios:
+            s, d = heap(16, DT["float"]), heap(16, DT["float"])
+            if ish.ishmem_float_sum_reduce(d, s, 0) != 0:  # nreduce == 0 still synchronises
+                fails.append(f"pe{pe} n=0 failed: {ish.last_error()}")
+            ins = [np.array([float(j + 1)], np.float32) for j in range(npes)]
+            hip.upload(s, ins[pe])
+            if ish.ishmem_float_sum_reduce(ish.ISHMEM_TEAM_WORLD, d, s, 1) != 0:
+                fails.append(f"pe{pe} n=1 failed")
+            else:
+                check("n=1", OPS["sum"], DT["float"], ins, hip.download(d, 1, np.float32))
+            # examples/5_pi_reduce.cpp shape: in-place size_sum_reduce of one element
+            cnt = np.array([1000 + pe], np.uint64)
+            hip.upload(s, cnt)
+            if ish.ishmem_size_sum_reduce(s, s, 1) != 0:
+                fails.append(f"pe{pe} pi-shape failed")
+            elif int(hip.download(s, 1, np.uint64)[0]) != sum(1000 + j for j in range(npes)):
+                fails.append(f"pe{pe} pi-shape wrong value")
+            ish.ishmem_free(d)
+            ish.ishmem_free(s)
+
+        if "stream" in scenarios:
+            n = 12345
+            ins = [oracle.fill_random(DT["int32"], 5 + j, n) for j in range(npes)]
+            s, d = heap(n, DT["int32"]), heap(n, DT["int32"])
+            ret = ish.ishmem_malloc(4)
+            hip.memset(ret, 0xFF, 4)
+            hip.upload(s, ins[pe])
+            st = hip.stream_create()
+            r = ish.ishmemx_int32_sum_reduce_on_stream(d, s, n, ret, st)
+            hip.stream_synchronize(st)
+            rv = int(hip.download(ret, 1, np.int32)[0])
+            if r != 0 or rv != 0:
+                fails.append(f"pe{pe} on_stream rc={r} ret={rv} {ish.last_error()}")
+            else:
+                check("on_stream", OPS["sum"], DT["int32"], ins, hip.download(d, n, np.int32))
+            hip.stream_destroy(st)
+            for p in (ret, d, s):
+                ish.ishmem_free(p)
+
+        if "staged" in scenarios:
+            # Host memory and device memory outside the heap go through the staging region.
+            n = 300_000
+            ins = [oracle.fill_random(DT["double"], 9 + j, n) for j in range(npes)]
+            src = np.ascontiguousarray(ins[pe])
+            out = np.zeros(n, np.float64)
+            r = ish.ishmem_double_max_reduce(out.ctypes.data, src.ctypes.data, n)
+            if r:
+                fails.append(f"pe{pe} host-staged rc={r} {ish.last_error()}")
+            else:
+                check("host-staged", OPS["max"], DT["double"], ins, out)
+            ds, dd = hip.malloc(n * 8), hip.malloc(n * 8)
+            hip.upload(ds, src)
+            r = ish.ishmem_double_sum_reduce(dd, ds, n)
+            if r:
+                fails.append(f"pe{pe} device-staged rc={r} {ish.last_error()}")
+            else:
+                check("device-staged", OPS["sum"], DT["double"], ins, hip.download(dd, n, np.float64))
+            hip.free(ds)
+            hip.free(dd)
+
+        if "team" in scenarios and npes >= 2:
+            # Strided team of the even PEs (examples/6_team_split_strided.cpp shape).
+            size = (npes + 1) // 2
+            r, team = ish.ishmem_team_split_strided(ish.ISHMEM_TEAM_WORLD, 0, 2, size)
+            if r:
+                fails.append(f"pe{pe} split rc={r} {ish.last_error()}")
+            n = 4099
+            members = list(range(0, npes, 2))
+            ins = {j: oracle.fill_random(DT["int64"], 40 + j, n) for j in members}
+            s, d = heap(n, DT["int64"]), heap(n, DT["int64"])
+            if team != ish.ISHMEM_TEAM_INVALID:
+                if ish.ishmem_team_my_pe(team) != members.index(pe):
+                    fails.append(f"pe{pe} team_my_pe wrong")
+                hip.upload(s, ins[pe])
+                r = ish.ishmem_int64_sum_reduce(team, d, s, n)
+                if r:
+                    fails.append(f"pe{pe} team reduce rc={r} {ish.last_error()}")
+                else:
+                    check("team", OPS["sum"], DT["int64"], [ins[j] for j in members], hip.download(d, n, np.int64))
+                ish.ishmem_team_destroy(team)
+            elif pe % 2 == 0:
+                fails.append(f"pe{pe} should be in the even team")
+            ish.ishmem_free(d)
+            ish.ishmem_free(s)
+
+        if "large" in scenarios:
+            # f32 sum over 64 Mi elements per PE (256 MiB): full-array comparison.
+            n = 64 << 20
+            s, d = heap(n, DT["float"]), heap(n, DT["float"])
+            ins = [oracle.fill_random(DT["float"], 0xABC + j, n) for j in range(npes)]
+            hip.upload(s, ins[pe])
+            r = ish.ishmem_float_sum_reduce(d, s, n)
+            if r:
+                fails.append(f"pe{pe} large rc={r} {ish.last_error()}")
+            else:
+                got = hip.download(d, n, np.float32)
+                ref = ins[0].copy()
+                for j in range(1, npes):
+                    ref += ins[j]  # canonical left-to-right fold, exactly the kernel's order
+                if not _bits_equal(got, ref):
+                    fails.append(f"pe{pe} large: {int(np.sum(got != ref))} elements differ")
+            ish.ishmem_free(d)
+            ish.ishmem_free(s)
+
+        if ish.lib().ishmemi_c_error_count() != 0:
+            fails.append(f"pe{pe} device barrier timeouts: {ish.lib().ishmemi_c_error_count()}")
+        ish.ishmem_barrier_all()
+        ish.ishmem_finalize()
+    except Exception:
+        fails.append(f"pe{pe} exception: {traceback.format_exc()}")
+    q.put((pe, fails))

@@ -1,0 +1,58 @@
+"""GPU parity of the multi-PE path (RS + AG over HIP IPC): 2 and 4 PEs as separate processes on
+the one GPU of the test box (the same protocol as one PE per MI355X over xGMI; the 8-GPU run is
+the driver's).  Every PE checks its dest against the oracle bit-for-bit (canonical team-order
+fold) and against MPICH's MPI_Allreduce golden output (ints / min / max bit-exact; FP sum/prod
+within (p-1)*u*sum|x_i| resp. (p-1)*u*|ref|)."""
+import multiprocessing as mp
+import uuid
+
+import pytest
+
+from tests import mp_worker
+
+pytestmark = pytest.mark.gpu
+
+ENV = {"ISHMEM_MAX_BLOCKS": 32, "ISHMEM_TIMEOUT_MS": 20000, "ISHMEM_SYMMETRIC_SIZE": "1G",
+       "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+
+
+def run_pes(npes: int, scenarios: list[str], timeout: float = 240.0, env: dict | None = None):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    key = f"t{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=mp_worker.run, args=(pe, npes, key, scenarios, q, {**ENV, **(env or {})}))
+             for pe in range(npes)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(npes):
+            pe, fails = q.get(timeout=timeout)
+            results[pe] = fails
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+                p.join()
+    assert len(results) == npes, f"only {len(results)} of {npes} PEs reported"
+    allfails = [f for pe in sorted(results) for f in results[pe]]
+    assert not allfails, "\n".join(allfails[:20])
+
+
+@pytest.mark.parametrize("npes", [2, 4])
+def test_all_ops_types_vs_oracle_and_mpich_golden(npes):
+    run_pes(npes, ["golden"])
+
+
+@pytest.mark.parametrize("npes", [2, 3])
+def test_inplace_offsets_edges(npes):
+    run_pes(npes, ["inplace", "offsets", "edge"])
+
+
+def test_stream_staged_team():
+    run_pes(4, ["stream", "staged", "team"])
+
+
+def test_large_f32_sum_256MiB_per_pe():
+    run_pes(2, ["large"], env={"ISHMEM_MAX_BLOCKS": 64})

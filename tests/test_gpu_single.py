@@ -1,0 +1,128 @@
+"""GPU parity of the single-GPU pieces of the path, through the C-ABI:
+  * the local combine unit dst = op(src_0..src_{k-1}) for every valid (op, dtype), ragged sizes
+    and misaligned operands, bit-exact against the oracle's fold (same left-to-right order);
+  * the 1-PE reduce (reference semantics: dest = source, reduce_impl.h:288-289) on heap, device
+    and host buffers, in place and via the stream API;
+  * the 1 GiB f32 combine (BASELINE config 2) compared in full.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+VALID = [(op, dt) for op in range(7) for dt in range(10) if oracle.valid(op, dt)]
+ONAMES = {v: k for k, v in oracle.OPS.items()}
+DNAMES = {v: k for k, v in oracle.DTYPES.items()}
+
+
+@pytest.fixture(scope="module")
+def ish():
+    import ishmem_amd
+    ishmem_amd.init(0, 1, 0, None)
+    yield ishmem_amd
+    ishmem_amd.ishmem_finalize()
+
+
+def _bits_equal(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8))
+
+
+@pytest.mark.parametrize("op,dt", VALID)
+def test_combine_parity_all_ops_types(ish, op, dt):
+    from ishmem_amd import hip
+    es = np.dtype(oracle.NP[dt]).itemsize
+    lo, hi = (0.5, 2.0) if op == oracle.OPS["prod"] else (-1.0, 1.0)
+    for k, n in [(1, 1000), (2, 1), (2, 17), (3, 4097), (8, 33333), (16, 1000)]:
+        srcs = [oracle.fill_random(dt, 31 * j + n, n, lo, hi) for j in range(k)]
+        dptrs = [hip.malloc(n * es) for _ in range(k)]
+        for p, s in zip(dptrs, srcs):
+            hip.upload(p, s)
+        dst = hip.malloc(n * es)
+        assert ish.combine(ONAMES[op], DNAMES[dt], dst, dptrs, n) == 0, ish.last_error()
+        hip.synchronize()
+        got = hip.download(dst, n, oracle.NP[dt])
+        ref = oracle.reduce_fold(op, dt, srcs, 0)
+        assert _bits_equal(got, ref), (op, dt, k, n)
+        for p in dptrs + [dst]:
+            hip.free(p)
+
+
+@pytest.mark.parametrize("dt", [0, 1, 2, 3, 8, 9])
+def test_combine_misaligned_operands(ish, dt):
+    from ishmem_amd import hip
+    es = np.dtype(oracle.NP[dt]).itemsize
+    op = oracle.OPS["sum"]
+    base = [hip.malloc(4096) for _ in range(3)]
+    for n in (1, 3, 16, 41, 200):
+        for offs in [(0, 0, 0), (es, es, es), (0, es, 2 * es), (3 * es, 0, 3 * es), (8, 8, 8)]:
+            offs = [o - (o % es) for o in offs]
+            srcs = [oracle.fill_random(dt, n + i, n) for i in range(2)]
+            hip.upload(base[0] + offs[0], srcs[0])
+            hip.upload(base[1] + offs[1], srcs[1])
+            assert ish.combine("sum", DNAMES[dt], base[2] + offs[2], [base[0] + offs[0], base[1] + offs[1]], n) == 0
+            hip.synchronize()
+            got = hip.download(base[2] + offs[2], n, oracle.NP[dt])
+            assert _bits_equal(got, oracle.reduce_fold(op, dt, srcs, 0)), (dt, n, offs)
+    for p in base:
+        hip.free(p)
+
+
+def test_single_pe_reduce_is_copy(ish):
+    from ishmem_amd import hip
+    n = 1_000_003
+    x = oracle.fill_random(oracle.DTYPES["float"], 3, n)
+    s = ish.ishmem_malloc(n * 4)
+    d = ish.ishmem_malloc(n * 4)
+    hip.upload(s, x)
+    assert ish.ishmem_float_sum_reduce(d, s, n) == 0
+    assert _bits_equal(hip.download(d, n, np.float32), x)
+    assert ish.ishmem_float_prod_reduce(s, s, n) == 0  # in place: unchanged
+    assert _bits_equal(hip.download(s, n, np.float32), x)
+    # host memory on one PE (reference: runtime allreduce on host pointers, reduce_impl.h:301-315)
+    out = np.zeros(n, np.float32)
+    assert ish.ishmem_float_max_reduce(out.ctypes.data, x.ctypes.data, n) == 0
+    assert _bits_equal(out, x)
+    # the stream variant writes *ret = 0
+    ret = ish.ishmem_malloc(4)
+    hip.memset(ret, 0xFF, 4)
+    st = hip.stream_create()
+    assert ish.ishmemx_float_sum_reduce_on_stream(d, s, n, ret, st) == 0
+    hip.stream_synchronize(st)
+    assert int(hip.download(ret, 1, np.int32)[0]) == 0
+    hip.stream_destroy(st)
+    for p in (ret, d, s):
+        ish.ishmem_free(p)
+
+
+def test_invalid_pairs_fail_cleanly(ish):
+    s = ish.ishmem_malloc(64)
+    assert ish.reduce("and", "float", s, s, 4) != 0
+    assert "invalid" in ish.last_error()
+    assert ish.lib().ishmemi_c_reduce(99, 5, 8, s, s, 4) != 0
+    ish.ishmem_free(s)
+
+
+def test_combine_1GiB_f32_sum_full_compare(ish):
+    from ishmem_amd import hip
+    n = 1 << 28  # 1 GiB of float32 (BASELINE config 2)
+    a = oracle.fill_random(oracle.DTYPES["float"], 11, n)
+    b = oracle.fill_random(oracle.DTYPES["float"], 12, n)
+    pa, pb, pd = hip.malloc(n * 4), hip.malloc(n * 4), hip.malloc(n * 4)
+    hip.upload(pa, a)
+    hip.upload(pb, b)
+    assert ish.combine("sum", "float", pd, [pa, pb], n) == 0
+    hip.synchronize()
+    got = hip.download(pd, n, np.float32)
+    assert _bits_equal(got, a + b)
+    # self-reduce (copy) at the same size
+    s = ish.ishmem_malloc(n * 4)
+    d = ish.ishmem_malloc(n * 4)
+    hip.memcpy(s, pa, n * 4)
+    assert ish.ishmem_float_sum_reduce(d, s, n) == 0
+    assert _bits_equal(hip.download(d, n, np.float32), a)
+    for p in (pa, pb, pd):
+        hip.free(p)
+    ish.ishmem_free(d)
+    ish.ishmem_free(s)
