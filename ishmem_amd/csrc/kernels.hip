@@ -301,47 +301,46 @@ __global__ __launch_bounds__(kBlock) void allreduce_kernel(ReduceArgs a)
 
 // ---------------------------------------------------------------------------------------------
 // Local fan-in combine: dst = op(src_0, ..., src_{k-1}), folded in source order.
+// Measured on MI355X (tools/stream_variants.hip, 1 GiB operands): a one-shot grid with ONE 16-B
+// item per thread and nontemporal loads + stores is the fastest shape (copy 6.59 TB/s = 82 %,
+// a + b 6.57 TB/s = 82 % of the 8 TB/s HBM peak); persistent grid-stride loops with 4-8 items
+// per thread reached only 63-73 %.  NS = 1 / 2 are specialised so every load is in flight
+// before the fold; NS = 0 handles any source count at run time.
 // ---------------------------------------------------------------------------------------------
-template <typename T, int OP, bool VEC>
-__global__ __launch_bounds__(kBlock) void fanin_kernel(FaninArgs a)
+template <typename I>
+__device__ __forceinline__ I nt_load(const I *p)
+{
+    if constexpr (sizeof(I) == 16) return __builtin_bit_cast(I, __builtin_nontemporal_load((const u32x4 *) p));
+    else return __builtin_nontemporal_load(p);
+}
+
+template <typename T, int OP, bool VEC, int NS>
+__global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
 {
     using Item = std::conditional_t<VEC, Vec<T>, T>;
     constexpr uint64_t IB = sizeof(Item);
-    const int tid = threadIdx.x;
-    const uint64_t G = gridDim.x;
     const uint64_t head_bytes = VEC ? a.head * sizeof(T) : 0;
-    for (uint64_t t0 = (uint64_t) blockIdx.x * kTile; t0 < a.nitems; t0 += G * kTile) {
-        Item acc[kUnroll];
-        const Item *s0 = (const Item *) (a.src[0] + head_bytes + t0 * IB);
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const uint64_t k = (uint64_t) u * kBlock + tid;
-            if (t0 + k < a.nitems) acc[u] = s0[k];
+    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
+    for (uint64_t i = (uint64_t) blockIdx.x * kFaninBlock + threadIdx.x; i < a.nitems; i += stride) {
+        const uint64_t off = head_bytes + i * IB;
+        Item acc;
+        if constexpr (NS == 1) {
+            acc = nt_load((const Item *) (a.src[0] + off));
+        } else if constexpr (NS == 2) {
+            const Item x0 = nt_load((const Item *) (a.src[0] + off));
+            const Item x1 = nt_load((const Item *) (a.src[1] + off));
+            acc = op1<T, OP>(x0, x1);
+        } else {
+            acc = nt_load((const Item *) (a.src[0] + off));
+            for (int j = 1; j < a.nsrc; ++j) acc = op1<T, OP>(acc, nt_load((const Item *) (a.src[j] + off)));
         }
-        for (int j = 1; j < a.nsrc; ++j) {
-            const Item *sj = (const Item *) (a.src[j] + head_bytes + t0 * IB);
-            Item x[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const uint64_t k = (uint64_t) u * kBlock + tid;
-                if (t0 + k < a.nitems) x[u] = sj[k];
-            }
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) acc[u] = op1<T, OP>(acc[u], x[u]);
-        }
-        Item *dp = (Item *) (a.dst + head_bytes + t0 * IB);
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const uint64_t k = (uint64_t) u * kBlock + tid;
-            if (t0 + k < a.nitems) nt_store(dp + k, acc[u]);
-        }
+        nt_store((Item *) (a.dst + off), acc);
     }
     if (VEC && blockIdx.x == 0) {
+        const int tid = threadIdx.x;
         const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
-        const bool do_head = (uint64_t) tid < a.head;
-        const bool do_tail = (uint64_t) tid < a.tail;
         for (int pass = 0; pass < 2; ++pass) {
-            if (pass == 0 ? !do_head : !do_tail) continue;
+            if ((uint64_t) tid >= (pass == 0 ? a.head : a.tail)) continue;
             const uint64_t e = pass == 0 ? (uint64_t) tid : tail_off + tid;
             T acc = ((const T *) a.src[0])[e];
             for (int j = 1; j < a.nsrc; ++j) acc = op1<T, OP>(acc, ((const T *) a.src[j])[e]);
@@ -370,11 +369,19 @@ hipError_t ar_t(bool vec, const ReduceArgs &a, int grid, hipStream_t s)
     return hipGetLastError();
 }
 
+template <typename T, int OP, bool VEC>
+void fi_ns(const FaninArgs &a, int grid, hipStream_t s)
+{
+    if (a.nsrc == 1) hipLaunchKernelGGL((fanin_kernel<T, OP, VEC, 1>), dim3(grid), dim3(kFaninBlock), 0, s, a);
+    else if (a.nsrc == 2) hipLaunchKernelGGL((fanin_kernel<T, OP, VEC, 2>), dim3(grid), dim3(kFaninBlock), 0, s, a);
+    else hipLaunchKernelGGL((fanin_kernel<T, OP, VEC, 0>), dim3(grid), dim3(kFaninBlock), 0, s, a);
+}
+
 template <typename T, int OP>
 hipError_t fi_t(bool vec, const FaninArgs &a, int grid, hipStream_t s)
 {
-    if (vec) hipLaunchKernelGGL((fanin_kernel<T, OP, true>), dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((fanin_kernel<T, OP, false>), dim3(grid), dim3(kBlock), 0, s, a);
+    if (vec) fi_ns<T, OP, true>(a, grid, s);
+    else fi_ns<T, OP, false>(a, grid, s);
     return hipGetLastError();
 }
 

@@ -226,7 +226,7 @@ Plan make_plan(const void *dst, const void *const *srcs, int nsrc, size_t n, siz
         pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t) max_blocks));
     } else {
         pl.items_per_chunk = pl.nitems;
-        const uint64_t g = (pl.nitems + tile - 1) / tile;
+        const uint64_t g = (pl.nitems + kFaninBlock - 1) / kFaninBlock;
         pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t) max_grid));
     }
     return pl;
@@ -289,7 +289,7 @@ int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)
     f.dst = (char *) dst;
     f.nsrc = 1;
     const void *srcs[1] = {src};
-    Plan pl = make_plan(dst, srcs, 1, bytes, 1, 1, 0, 2048);
+    Plan pl = make_plan(dst, srcs, 1, bytes, 1, 1, 0, kFaninMaxGrid);
     f.head = pl.head;
     f.nitems = pl.nitems;
     f.tail = pl.tail;
@@ -773,7 +773,7 @@ int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int
     }
     f.dst = (char *) dst;
     f.nsrc = nsrc;
-    Plan pl = make_plan(dst, srcs, nsrc, n, dtype_size(dtype), 1, 0, 2048);
+    Plan pl = make_plan(dst, srcs, nsrc, n, dtype_size(dtype), 1, 0, kFaninMaxGrid);
     f.head = pl.head;
     f.nitems = pl.nitems;
     f.tail = pl.tail;

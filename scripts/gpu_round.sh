@@ -1,0 +1,47 @@
+#!/usr/bin/env bash
+# GPU-box driver for one measurement round.  Each GPU step has its own time limit; a fault,
+# abort, segfault or timeout (exit 124/134/137/139) ends the script at once — no retries.
+# Usage: scripts/gpu_round.sh TAG [steps...]   steps: smoke single multi bench prof pmc
+set -u
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG="${1:-r01}"; shift || true
+STEPS="${*:-smoke single multi bench prof}"
+OUT="$R/gpurun_out/$TAG"
+mkdir -p "$OUT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+cd "$R"
+
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() {  # name seconds cmd...
+  local name="$1" secs="$2"; shift 2
+  echo "=== $name ($(date +%T))" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL rc=$rc in $name: stopping" | tee -a "$OUT/steps.log"; exit $rc; fi
+  return 0
+}
+
+rocminfo 2>/dev/null | grep -m3 -E "gfx950|Marketing" > "$OUT/device.txt" || true
+nproc > "$OUT/host.txt"; lscpu | grep -m1 "Model name" >> "$OUT/host.txt" || true
+
+for s in $STEPS; do
+  case "$s" in
+    smoke)  run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    single) run pytest_single 900 python -m pytest tests/test_gpu_single.py -m gpu -x -q -p no:cacheprovider ;;
+    multi)  run pytest_multi 1200 python -m pytest tests/test_gpu_multi.py -m gpu -x -q -p no:cacheprovider ;;
+    bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    prof)   cd /tmp && export TMPDIR=/tmp
+            run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+                python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline
+            cd "$R" ;;
+    pmc)    cd /tmp && export TMPDIR=/tmp
+            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
+                python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
+            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
+                python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
+            cd "$R" ;;
+  esac
+done
+echo "done" >> "$OUT/steps.log"
