@@ -79,7 +79,10 @@ def main() -> None:
     import ishmem_amd as ish
     from ishmem_amd import hip
 
-    ish.init(rank, world, local_rank, key)
+    # ISHMEM_BENCH_SAME_DEVICE=1 (development only): every rank on device 0, to measure kernel
+    # overheads of the multi-PE path on a one-GPU box.  Never used for reported numbers.
+    device = 0 if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else local_rank
+    ish.init(rank, world, device, key)
     n = (args.mib << 20) // 4
     B = n * 4
     src = ish.ishmem_malloc(B)
@@ -188,7 +191,8 @@ def main() -> None:
                                    f"symmetric-heap device buffers", "nreduce": n,
                        "bytes_per_pe": B, "pes": world,
                        "parallelism": "1 PE self-reduce" if world == 1 else f"direct RS+AG over {world} PEs"},
-            "kernel_ms": kern_ms, "roofline": roof, "cpu_baseline": cpu, **extra,
+            "kernel_ms": kern_ms,
+            **({"dev_same_device": True} if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else {}), "roofline": roof, "cpu_baseline": cpu, **extra,
         }
         print(json.dumps(line))
     if dist is not None:

@@ -261,8 +261,12 @@ __global__ __launch_bounds__(kBlock) void allreduce_kernel(ReduceArgs a)
 
     // ---- all-gather: pull every other member's reduced chunk from its dest ----
     if (ok) {
-        for (int jj = 1; jj < p; ++jj) {
-            const int j = (me + jj) % p;  // stagger so the members' pulls spread over the links
+        for (int k = 0; k < p - 1; ++k) {
+            // Peer order rotated by workgroup index: at any instant the workgroups of this PE
+            // pull from all p-1 peers at once, i.e. over all p-1 xGMI links, instead of every
+            // workgroup draining the same peer (one link) before moving to the next.  The tiles
+            // a workgroup pulls are still exactly those its partner workgroup b produced.
+            const int j = (me + 1 + (b + k) % (p - 1)) % p;
             const uint64_t cs = min((uint64_t) j * a.items_per_chunk, a.nitems);
             const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
             for (uint64_t t0 = cs + (uint64_t) b * kTile; t0 < ce; t0 += G * kTile) {

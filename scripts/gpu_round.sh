@@ -32,6 +32,12 @@ for s in $STEPS; do
     single) run pytest_single 900 python -m pytest tests/test_gpu_single.py -m gpu -x -q -p no:cacheprovider ;;
     multi)  run pytest_multi 1200 python -m pytest tests/test_gpu_multi.py -m gpu -x -q -p no:cacheprovider ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    local2) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-256} run bench_local2 600 python -m torch.distributed.run \
+                --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 \
+                --steps 10 --warmup 3 --mib ${MIB:-1024} ;;
+    local4) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-128} run bench_local4 600 python -m torch.distributed.run \
+                --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 4 \
+                --steps 10 --warmup 3 --mib ${MIB:-512} ;;
     prof)   cd /tmp && export TMPDIR=/tmp
             run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                 python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Copy a gpurun profiling run into profiles/ and write profiles/pmc_summary.json.
+
+  python tools/summarize_profiles.py gpurun_out/<tag> <round-tag>
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half of
+the bytes of a wide (16 B/lane) coalesced stream on gfx950, so it is doubled; WRITE_SIZE (KB) is
+exact for 16-B streaming stores.  FETCH_SIZE and WRITE_SIZE come from separate --pmc passes.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import shutil
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+PROFILES = ROOT / "profiles"
+
+TAGS = {  # kernel-name fragment -> (summary key, algorithmic bytes per launch / payload B)
+    "fanin_kernel<unsigned char, 1, true, 1>": ("copy_1pe", 2),
+    "fanin_kernel<float, 5, true, 2>": ("combine2_1pe", 3),
+}
+
+
+def per_kernel(path: Path, counter: str) -> dict[str, list[float]]:
+    out: dict[str, list[float]] = {}
+    for r in csv.DictReader(path.open()):
+        if r["Counter_Name"] == counter:
+            out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    return out
+
+
+def main() -> None:
+    src, tag = Path(sys.argv[1]), sys.argv[2]
+    payload = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 30
+    PROFILES.mkdir(exist_ok=True)
+    for sub, name in [("prof/run_kernel_stats.csv", f"{tag}_kernel_stats.csv"),
+                      ("prof/run_kernel_trace.csv", f"{tag}_kernel_trace.csv"),
+                      ("pmc_fetch/run_counter_collection.csv", f"{tag}_pmc_fetch_size.csv"),
+                      ("pmc_write/run_counter_collection.csv", f"{tag}_pmc_write_size.csv")]:
+        if (src / sub).exists():
+            shutil.copy(src / sub, PROFILES / name)
+    summary_path = PROFILES / "pmc_summary.json"
+    summary = json.loads(summary_path.read_text()) if summary_path.exists() else {}
+    fetch = per_kernel(src / "pmc_fetch/run_counter_collection.csv", "FETCH_SIZE")
+    write = per_kernel(src / "pmc_write/run_counter_collection.csv", "WRITE_SIZE")
+    for frag, (key, mult) in TAGS.items():
+        f = [v for k, v in fetch.items() if frag in k]
+        w = [v for k, v in write.items() if frag in k]
+        if not f or not w:
+            continue
+        fk, wk = sum(f[0]) / len(f[0]), sum(w[0]) / len(w[0])
+        hbm = (2.0 * fk + wk) * 1024.0
+        summary[key] = {"kernel": frag, "payload_bytes": payload, "fetch_size_kb_raw": fk,
+                        "write_size_kb": wk, "hbm_bytes_per_launch": hbm,
+                        "algorithmic_bytes_per_launch": mult * payload,
+                        "traffic_over_algorithmic": hbm / (mult * payload),
+                        "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streams)", "source": tag}
+    summary_path.write_text(json.dumps(summary, indent=2) + "\n")
+    print(json.dumps(summary, indent=2))
+
+
+if __name__ == "__main__":
+    main()
