@@ -104,6 +104,8 @@ struct State {
 
     char *staging = nullptr;  // symmetric staging region for non-heap / host buffers
     size_t staging_bytes = 0;
+    hipStream_t copy_in = nullptr, copy_out = nullptr;  // staging pipeline streams
+    hipEvent_t ev_in[2] = {}, ev_red[2] = {}, ev_out[2] = {};
 
     Team teams[kMaxTeams];
     int max_blocks = kMaxBlocks;
@@ -325,6 +327,52 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     return 0;
 }
 
+// Non-symmetric buffers (host memory, or device memory outside the heap): a 3-stage pipeline
+// through two halves of the symmetric staging region.  Chunk k: copy-in on the `in` stream,
+// in-place collective on the caller's stream, copy-out on the `out` stream; chunk k+1's copy-in
+// and chunk k-1's copy-out overlap chunk k's collective (PCIe is full duplex).  Replaces the
+// synchronous 64 KiB bounce loop ishmemi_generic_op_reduce (src/collectives/reduce_impl.h:186-228).
+int reduce_staged(State &s, int team, int op, int dt, void *dst, const void *src, size_t n,
+                  int *ret, hipStream_t st)
+{
+    const size_t es = dtype_size(dt);
+    const size_t slot_bytes = (s.staging_bytes / 2) & ~(kHeapAlign - 1);
+    const size_t chunk = (slot_bytes / es) & ~size_t(63);
+    if (chunk == 0) return fail("reduce: staging region too small");
+    if (!s.copy_in) {
+        HIP_TRY(hipStreamCreateWithFlags(&s.copy_in, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&s.copy_out, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) {
+            HIP_TRY(hipEventCreateWithFlags(&s.ev_in[i], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s.ev_red[i], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s.ev_out[i], hipEventDisableTiming));
+        }
+    }
+    HIP_TRY(hipEventRecord(s.ev_red[0], st));  // copy-ins start after the caller's prior work
+    HIP_TRY(hipStreamWaitEvent(s.copy_in, s.ev_red[0], 0));
+    bool used[2] = {false, false};
+    for (size_t off = 0, k = 0; off < n; off += chunk, ++k) {
+        const int sl = (int) (k & 1);
+        char *buf = s.staging + (size_t) sl * slot_bytes;
+        const size_t m = std::min(chunk, n - off);
+        if (used[sl]) HIP_TRY(hipStreamWaitEvent(s.copy_in, s.ev_out[sl], 0));  // slot drained
+        HIP_TRY(hipMemcpyAsync(buf, (const char *) src + off * es, m * es, hipMemcpyDefault,
+                               s.copy_in));
+        HIP_TRY(hipEventRecord(s.ev_in[sl], s.copy_in));
+        HIP_TRY(hipStreamWaitEvent(st, s.ev_in[sl], 0));
+        // One PE: the in-place reduce of the staged chunk is the identity (reduce_impl.h:288-289).
+        if (s.teams[team].size > 1 && reduce_heap(s, team, op, dt, buf, buf, m, ret, st)) return 1;
+        HIP_TRY(hipEventRecord(s.ev_red[sl], st));
+        HIP_TRY(hipStreamWaitEvent(s.copy_out, s.ev_red[sl], 0));
+        HIP_TRY(hipMemcpyAsync((char *) dst + off * es, buf, m * es, hipMemcpyDefault, s.copy_out));
+        HIP_TRY(hipEventRecord(s.ev_out[sl], s.copy_out));
+        used[sl] = true;
+    }
+    for (int sl = 0; sl < 2; ++sl)  // the caller's stream completes only after every copy-out
+        if (used[sl]) HIP_TRY(hipStreamWaitEvent(st, s.ev_out[sl], 0));
+    return 0;
+}
+
 int team_sync_locked(State &s, int team, hipStream_t st, int *ret)
 {
     Team &t = s.teams[team];
@@ -357,7 +405,9 @@ int reduce_impl(int team, int op, int dt, void *dst, const void *src, size_t n, 
         if (n > 0 && dst != src) {
             const Kind kd = classify(s, dst), ks = classify(s, src);
             if (kd == Kind::Host || ks == Kind::Host) {
-                HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
+                // Host buffers take the same HBM-staged pipeline as on a multi-PE team, so the
+                // path's host-to-host rate is the one reported in DESIGN.md.
+                if (reduce_staged(s, team, op, dt, dst, src, n, ret, st)) return 1;
             } else if (launch_copy(dst, src, bytes, st)) {
                 return 1;
             }
@@ -369,19 +419,7 @@ int reduce_impl(int team, int op, int dt, void *dst, const void *src, size_t n, 
     } else if (in_heap(s, dst) && in_heap(s, src)) {
         if (reduce_heap(s, team, op, dt, dst, src, n, ret, st)) return 1;
     } else {
-        // Non-symmetric buffers (host memory, or device memory outside the heap): stage each
-        // chunk through the symmetric staging region, reduce it in place there, copy it out.
-        // Replaces the 64 KiB host bounce loop ishmemi_generic_op_reduce (reduce_impl.h:186-228).
-        const size_t chunk = (s.staging_bytes / es) & ~size_t(63);
-        if (chunk == 0) return fail("reduce: staging region too small");
-        for (size_t off = 0; off < n; off += chunk) {
-            const size_t m = std::min(chunk, n - off);
-            HIP_TRY(hipMemcpyAsync(s.staging, (const char *) src + off * es, m * es,
-                                   hipMemcpyDefault, st));
-            if (reduce_heap(s, team, op, dt, s.staging, s.staging, m, ret, st)) return 1;
-            HIP_TRY(hipMemcpyAsync((char *) dst + off * es, s.staging, m * es, hipMemcpyDefault,
-                                   st));
-        }
+        if (reduce_staged(s, team, op, dt, dst, src, n, ret, st)) return 1;
     }
     if (blocking) {
         HIP_TRY(hipStreamSynchronize(st));
@@ -500,7 +538,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         t.my_idx = pe;
     }
     // Symmetric staging region (first allocation on every PE, hence the same offset).
-    s.staging_bytes = parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 64 << 20);
+    s.staging_bytes = parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20);
     s.staging = (char *) heap_alloc(s, s.staging_bytes, kHeapAlign);
     if (!s.staging) return 1;
     s.initialized = true;
@@ -563,6 +601,16 @@ int ishmemi_c_finalize(void)
         }
         s.boot.barrier(err);
         s.boot.detach();
+    }
+    if (s.copy_in) {
+        hipStreamDestroy(s.copy_in);
+        hipStreamDestroy(s.copy_out);
+        for (int i = 0; i < 2; ++i) {
+            hipEventDestroy(s.ev_in[i]);
+            hipEventDestroy(s.ev_red[i]);
+            hipEventDestroy(s.ev_out[i]);
+        }
+        s.copy_in = s.copy_out = nullptr;
     }
     hipFree(s.heap);
     hipFree(s.flags);
