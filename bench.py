@@ -61,6 +61,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--nelems", type=int, default=0, help="override: float32 elements per PE")
+    ap.add_argument("--rccl", action="store_true",
+                    help="N>1: also time RCCL all_reduce on the same payload (comparison only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -85,7 +88,7 @@ def main() -> None:
     # overheads of the multi-PE path on a one-GPU box.  Never used for reported numbers.
     device = 0 if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else local_rank
     ish.init(rank, world, device, key)
-    n = (args.mib << 20) // 4
+    n = args.nelems if args.nelems > 0 else (args.mib << 20) // 4
     B = n * 4
     src = ish.ishmem_malloc(B)
     dst = ish.ishmem_malloc(B)
@@ -205,13 +208,39 @@ def main() -> None:
         except Exception as ex:  # reported, never fatal for the main measurement
             extra["e2e_host"] = {"error": str(ex)}
 
+    if world > 1 and (args.rccl or os.environ.get("ISHMEM_BENCH_RCCL") == "1"):
+        # Comparison only: RCCL (torch "nccl" backend) all_reduce of the same payload.
+        try:
+            import torch
+            torch.cuda.set_device(device)
+            pg = dist.new_group(backend="nccl")
+            buf = torch.ones(n, dtype=torch.float32, device="cuda")
+            for _ in range(3):
+                dist.all_reduce(buf, group=pg)
+            torch.cuda.synchronize()
+            dist.barrier()
+            k = args.steps
+            tr0 = time.perf_counter()
+            for _ in range(k):
+                dist.all_reduce(buf, group=pg)
+            torch.cuda.synchronize()
+            tr = time.perf_counter() - tr0
+            tt = torch.tensor([tr], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            tr = float(tt[0])
+            extra["rccl_allreduce"] = {"value": world * B / GiB / (tr / k), "unit": "GiB/s",
+                                       "ms_per_step": tr / k * 1000.0}
+            del buf
+        except Exception as ex:
+            extra["rccl_allreduce"] = {"error": str(ex)}
+
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         import oracle  # CPU baseline leg only: the reference's host-proxy reduce, restated
         reps = 3
         t_cpu = oracle.host_proxy_time(oracle.OPS["sum"], oracle.DTYPES["float"], n, 1, reps)
         cpu = {"value": B / GiB / t_cpu, "unit": "GiB/s", "cores": 1, "kind": "port",
-               "sample": f"full workload: 1 PE f32 sum-reduce of {args.mib} MiB through 64 KiB host "
+               "sample": f"full workload: 1 PE f32 sum-reduce of {B / 2**20:g} MiB through 64 KiB host "
                          f"bounce chunks (reduce_impl.h:186-228), best of {reps}"}
 
     ish.ishmem_free(dst)
@@ -224,7 +253,7 @@ def main() -> None:
             "value": value, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"float32 sum-reduce, {args.mib} MiB per PE, {world} PE(s), "
+            "config": {"workload": f"float32 sum-reduce, {B / 2**20:g} MiB per PE, {world} PE(s), "
                                    f"symmetric-heap device buffers", "nreduce": n,
                        "bytes_per_pe": B, "pes": world,
                        "parallelism": "1 PE self-reduce" if world == 1 else f"direct RS+AG over {world} PEs"},

@@ -18,7 +18,11 @@ INCLUDE = ROOT / "include"
 BUILD = ROOT / "build" / "native"
 LIB = PKG / "libishmem_amd.so"
 
-SOURCES = ["kernels.hip", "runtime.cpp", "bootstrap.cpp"]
+# (source, object stem, extra flags): kernels_op.hip is compiled once per reduction op so the
+# ~350 kernel instantiations build in parallel.
+SOURCES = [("kernels.hip", "kernels", []), ("runtime.cpp", "runtime", []),
+           ("bootstrap.cpp", "bootstrap", [])] + [
+    ("kernels_op.hip", f"kernels_op{op}", [f"-DISHMEMI_KOP={op}"]) for op in range(7)]
 ARCH = os.environ.get("ISHMEM_OFFLOAD_ARCH", "gfx950")
 
 
@@ -49,10 +53,10 @@ def build(force: bool = False, verbose: bool = False) -> Path:
               "-Wall", "-Wno-unused-function"]
     objs = []
     procs = []
-    for src in SOURCES:
-        obj = BUILD / (Path(src).stem + ".o")
+    for src, stem, extra in SOURCES:
+        obj = BUILD / (stem + ".o")
         objs.append(obj)
-        cmd = [hipcc, *common, "-c", str(CSRC / src), "-o", str(obj)]
+        cmd = [hipcc, *common, *extra, "-c", str(CSRC / src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -1,446 +1,49 @@
-// ishmem_amd — HIP kernels of the reduction-collective hot path (gfx950 / MI355X).
-//
-// What the reference does (src/collectives/reduce_impl.h):
-//   * reduce_op<T,OP> (:62-102): FP max/min = fmax/fmin, sum +=, prod *=; ints & | ^ max min + *.
-//   * vector_reduce / vector_reduce_work_group (:105-183): d[i] = op(d[i], s[i]) with 16-wide
-//     vectors, run by ONE work-item or ONE work-group.
-//   * ishmemi_sub_reduce (:232-256): team barrier, then for every other PE in team order fold
-//     that PE's whole source into dest (p-1 full passes, each over the peer link), barrier.
-//
-// What this file does instead (MI355X-first, not a translation):
-//   * fanin_kernel: dst = op(src_0, ..., src_{k-1}) over 16-B vectors, every CU busy, all sources
-//     streamed once (the local combine unit; with k = 1 it is the p = 1 self-reduce copy).
-//   * allreduce_kernel: ONE launch per collective, direct reduce-scatter + all-gather across the
-//     team.  PE c folds chunk c of every member's source (pulled over xGMI with system-coherent
-//     loads) in canonical team order 0..p-1 and writes its own dest; after a per-workgroup
-//     barrier every PE pulls the other reduced chunks from the peers' dests.  Each PE's link
-//     ingress is 2(p-1)/p * B spread over p-1 links, vs (p-1) * B serialised over peers in the
-//     reference loop.  Folding in canonical order makes every PE's result bit-identical (the
-//     reference's results differ between PEs for FP, docs/source/collectives.rst:1241-1244) and
-//     equal to the reference's PE-0 result and to its tester's check pattern
-//     (test/unit/reduce_sum.cpp:203-224).
-//   * The barriers replace ishmemi_team_sync's psync counters (src/collectives/sync_impl.h:30-69)
-//     with epoch-tagged flags in fine-grained memory, paired per workgroup index: workgroup b
-//     of every PE processes the same tiles of every chunk, so a barrier between the workgroups
-//     with index b is all the ordering the data needs (no grid-wide sync).  All remote
-//     accesses are LOADS (pull), so no PE's L2 can hold stale copies of bytes a peer wrote.
-#include <type_traits>
-
-#include "kernels.h"
+// ishmem_amd — launch dispatch of the reduction-collective kernels (see kernels_impl.h for the
+// kernels and their design notes; kernels_op.hip instantiates them once per op).
+#include "kernels_impl.h"
 
 namespace ishmemi {
-namespace {
 
-// sc0|sc1 cache policy on gfx950 buffer instructions = system-coherent access.
-constexpr int kSysCoherent = 17;
-constexpr uint64_t kTile = (uint64_t) kBlock * kUnroll;  // items per tile
-
-template <typename T>
-struct alignas(16) Vec {
-    T e[16 / sizeof(T)];
-};
-
-template <typename T>
-struct WideOf {
-    using type = uint32_t;
-};
-template <>
-struct WideOf<uint64_t> {
-    using type = uint64_t;
-};
-
-// reduce_op semantics of src/collectives/reduce_impl.h:83-102 on canonical types.
-template <typename T, int OP>
-__device__ __forceinline__ T op1(T a, T b)
-{
-    if constexpr (OP == ISHMEMI_OP_AND) return (T) (a & b);
-    else if constexpr (OP == ISHMEMI_OP_OR) return (T) (a | b);
-    else if constexpr (OP == ISHMEMI_OP_XOR) return (T) (a ^ b);
-    else if constexpr (OP == ISHMEMI_OP_MAX) {
-        if constexpr (std::is_same_v<T, float>) return fmaxf(a, b);
-        else if constexpr (std::is_same_v<T, double>) return fmax(a, b);
-        else return (a < b) ? b : a;
-    } else if constexpr (OP == ISHMEMI_OP_MIN) {
-        if constexpr (std::is_same_v<T, float>) return fminf(a, b);
-        else if constexpr (std::is_same_v<T, double>) return fmin(a, b);
-        else return (b < a) ? b : a;
-    } else if constexpr (OP == ISHMEMI_OP_SUM) {
-        if constexpr (std::is_floating_point_v<T>) return a + b;
-        else return (T) ((typename WideOf<T>::type) a + (typename WideOf<T>::type) b);
-    } else {
-        if constexpr (std::is_floating_point_v<T>) return a * b;
-        else return (T) ((typename WideOf<T>::type) a * (typename WideOf<T>::type) b);
-    }
-}
-
-template <typename T, int OP>
-__device__ __forceinline__ Vec<T> op1(const Vec<T> &a, const Vec<T> &b)
-{
-    Vec<T> r;
-#pragma unroll
-    for (int i = 0; i < (int) (16 / sizeof(T)); ++i) r.e[i] = op1<T, OP>(a.e[i], b.e[i]);
-    return r;
-}
-
-__device__ __forceinline__ const char *uniform_ptr(const char *p)
-{
-    const uint64_t v = (uint64_t) p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t) v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t) (v >> 32));
-    return (const char *) (((uint64_t) hi << 32) | lo);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const char *uniform_base)
-{
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(uniform_base), (short) 0,
-                                             0x7FFFFFFF, 0x00020000);
-}
-
-// System-coherent (sc0 sc1) load of one item from a peer's memory.
-template <typename I>
-__device__ __forceinline__ I cload(__amdgpu_buffer_rsrc_t r, uint32_t off)
-{
-    if constexpr (sizeof(I) == 16) {
-        return __builtin_bit_cast(I, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSysCoherent));
-    } else if constexpr (sizeof(I) == 8) {
-        return __builtin_bit_cast(I, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kSysCoherent));
-    } else if constexpr (sizeof(I) == 4) {
-        return __builtin_bit_cast(I, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kSysCoherent));
-    } else if constexpr (sizeof(I) == 2) {
-        return __builtin_bit_cast(I, __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, kSysCoherent));
-    } else {
-        return __builtin_bit_cast(I, __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, kSysCoherent));
-    }
-}
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// Streaming store that does not keep the line in L2 / Infinity Cache (output is not re-read).
-template <typename I>
-__device__ __forceinline__ void nt_store(I *p, const I &v)
-{
-    if constexpr (sizeof(I) == 16) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (u32x4 *) p);
-    else __builtin_nontemporal_store(v, p);
-}
-
-__device__ __forceinline__ uint32_t *flag_slot(uint32_t *base, int phase, int block)
-{
-    return base + ((size_t) phase * kMaxBlocks + (size_t) block) * kMaxPes;
-}
-
-// Pairwise barrier between the workgroups with index `block` on every team member.
-// Replaces ishmemi_team_sync (src/collectives/sync_impl.h:30-69): instead of p remote
-// fetch-adds on one psync word and a spin to `size`, member me stores the call's epoch into
-// its own slot of every peer's flag row, then polls its local row until every peer's slot
-// holds the epoch (wrap-safe compare).  Called by ALL threads of the block; returns false on
-// timeout (recorded in *err) so the caller can drain instead of hanging the GPU.
-__device__ bool pe_barrier(const ReduceArgs &a, int phase, int block)
-{
-    __shared__ int s_ok;
-    // Every storing wave drains its stores, then one wave publishes (Guideline 16, R1).
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        const int p = a.p, me = a.me;
-        // System-scope release: write back this XCD's L2 so the bytes this workgroup wrote are
-        // visible to peers' coherent loads.  The asm wait guards against the compiler dropping
-        // the wait after buffer_wbl2 (MI355X_MICROARCH.md, compiler hazard).
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-            for (int j = 0; j < p; ++j) {
-                if (j == me) continue;
-                __hip_atomic_store(flag_slot(a.peer_flags[j], phase, block) + me, a.epoch,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-        uint32_t *row = flag_slot(a.my_flags, phase, block);
-        bool done = (lane >= p) || (lane == me);
-        bool timed_out = false;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (!__all(done)) {
-            if (!done) {
-                const uint32_t v =
-                    __hip_atomic_load(row + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                done = (int32_t) (v - a.epoch) >= 0;
-            }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-                timed_out = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        // System-scope acquire: drop this CU's L1 / non-coherent L2 lines before reading peers.
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        if (lane == 0) {
-            s_ok = !timed_out;
-            if (timed_out)
-                __hip_atomic_fetch_or(a.err, 1u << phase, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-    __syncthreads();
-    return s_ok != 0;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Multi-PE reduce-scatter + all-gather (one launch per collective).
-// ---------------------------------------------------------------------------------------------
-template <typename T, int OP, bool VEC>
-__global__ __launch_bounds__(kBlock) void allreduce_kernel(ReduceArgs a)
-{
-    using Item = std::conditional_t<VEC, Vec<T>, T>;
-    constexpr uint64_t IB = sizeof(Item);
-    const int tid = threadIdx.x;
-    const int b = blockIdx.x;
-    const uint64_t G = gridDim.x;
-    const int p = a.p, me = a.me;
-    const uint64_t head_bytes = VEC ? a.head * sizeof(T) : 0;
-    bool ok = pe_barrier(a, kPhaseStart, b);
-
-    // ---- reduce-scatter: fold chunk `me` of every member's source, canonical team order ----
-    if (ok) {
-        const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
-        const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
-        for (uint64_t t0 = cs + (uint64_t) b * kTile; t0 < ce; t0 += G * kTile) {
-            Item acc[kUnroll];
-            for (int j = 0; j < p; ++j) {
-                const char *base = uniform_ptr(a.src[j] + head_bytes + t0 * IB);
-                Item x[kUnroll];
-                if (j == me) {
-                    const Item *lp = (const Item *) base;
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) {
-                        const uint64_t k = (uint64_t) u * kBlock + tid;
-                        if (t0 + k < ce) x[u] = lp[k];
-                    }
-                } else {
-                    const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) {
-                        const uint64_t k = (uint64_t) u * kBlock + tid;
-                        if (t0 + k < ce) x[u] = cload<Item>(r, (uint32_t) (k * IB));
-                    }
-                }
-                if (j == 0) {
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) acc[u] = x[u];
-                } else {
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) acc[u] = op1<T, OP>(acc[u], x[u]);
-                }
-            }
-            Item *dp = (Item *) (a.dst + head_bytes + t0 * IB);
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const uint64_t k = (uint64_t) u * kBlock + tid;
-                if (t0 + k < ce) dp[k] = acc[u];
-            }
-        }
-        // Unaligned head (owned by member 0) and tail (owned by member p-1), element-wise.
-        if (VEC && b == 0) {
-            const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
-            const bool do_head = (me == 0) && ((uint64_t) tid < a.head);
-            const bool do_tail = (me == p - 1) && ((uint64_t) tid < a.tail);
-            if (do_head || do_tail) {
-                const uint64_t e = do_head ? (uint64_t) tid : tail_off + tid;
-                T acc = T();
-                for (int j = 0; j < p; ++j) {
-                    T x;
-                    if (j == me) x = ((const T *) a.src[j])[e];
-                    else x = cload<T>(make_rsrc(uniform_ptr(a.src[j])), (uint32_t) (e * sizeof(T)));
-                    acc = (j == 0) ? x : op1<T, OP>(acc, x);
-                }
-                ((T *) a.dst)[e] = acc;
-            }
-        }
-    }
-
-    ok = ok && pe_barrier(a, kPhaseMid, b);
-
-    // ---- all-gather: pull every other member's reduced chunk from its dest ----
-    if (ok) {
-        for (int k = 0; k < p - 1; ++k) {
-            // Peer order rotated by workgroup index: at any instant the workgroups of this PE
-            // pull from all p-1 peers at once, i.e. over all p-1 xGMI links, instead of every
-            // workgroup draining the same peer (one link) before moving to the next.  The tiles
-            // a workgroup pulls are still exactly those its partner workgroup b produced.
-            const int j = (me + 1 + (b + k) % (p - 1)) % p;
-            const uint64_t cs = min((uint64_t) j * a.items_per_chunk, a.nitems);
-            const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
-            for (uint64_t t0 = cs + (uint64_t) b * kTile; t0 < ce; t0 += G * kTile) {
-                const __amdgpu_buffer_rsrc_t r =
-                    make_rsrc(uniform_ptr(a.dstp[j] + head_bytes + t0 * IB));
-                Item x[kUnroll];
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const uint64_t k = (uint64_t) u * kBlock + tid;
-                    if (t0 + k < ce) x[u] = cload<Item>(r, (uint32_t) (k * IB));
-                }
-                Item *dp = (Item *) (a.dst + head_bytes + t0 * IB);
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const uint64_t k = (uint64_t) u * kBlock + tid;
-                    if (t0 + k < ce) dp[k] = x[u];
-                }
-            }
-            if (VEC && b == 0) {
-                const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
-                const bool do_head = (j == 0) && ((uint64_t) tid < a.head);
-                const bool do_tail = (j == p - 1) && ((uint64_t) tid < a.tail);
-                if (do_head || do_tail) {
-                    const uint64_t e = do_head ? (uint64_t) tid : tail_off + tid;
-                    ((T *) a.dst)[e] =
-                        cload<T>(make_rsrc(uniform_ptr(a.dstp[j])), (uint32_t) (e * sizeof(T)));
-                }
-            }
-        }
-    }
-
-    // ---- end: peers have finished pulling from my dest before anyone returns ----
-    ok = ok && pe_barrier(a, kPhaseEnd, b);
-    if (b == 0 && tid == 0 && a.ret) *a.ret = ok ? 0 : 1;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Local fan-in combine: dst = op(src_0, ..., src_{k-1}), folded in source order.
-// Measured on MI355X (tools/stream_variants.hip, 1 GiB operands): a one-shot grid with ONE 16-B
-// item per thread and nontemporal loads + stores is the fastest shape (copy 6.59 TB/s = 82 %,
-// a + b 6.57 TB/s = 82 % of the 8 TB/s HBM peak); persistent grid-stride loops with 4-8 items
-// per thread reached only 63-73 %.  NS = 1 / 2 are specialised so every load is in flight
-// before the fold; NS = 0 handles any source count at run time.
-// ---------------------------------------------------------------------------------------------
-template <typename I>
-__device__ __forceinline__ I nt_load(const I *p)
-{
-    if constexpr (sizeof(I) == 16) return __builtin_bit_cast(I, __builtin_nontemporal_load((const u32x4 *) p));
-    else return __builtin_nontemporal_load(p);
-}
-
-template <typename T, int OP, bool VEC, int NS>
-__global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
-{
-    using Item = std::conditional_t<VEC, Vec<T>, T>;
-    constexpr uint64_t IB = sizeof(Item);
-    const uint64_t head_bytes = VEC ? a.head * sizeof(T) : 0;
-    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
-    for (uint64_t i = (uint64_t) blockIdx.x * kFaninBlock + threadIdx.x; i < a.nitems; i += stride) {
-        const uint64_t off = head_bytes + i * IB;
-        Item acc;
-        if constexpr (NS == 1) {
-            acc = nt_load((const Item *) (a.src[0] + off));
-        } else if constexpr (NS == 2) {
-            const Item x0 = nt_load((const Item *) (a.src[0] + off));
-            const Item x1 = nt_load((const Item *) (a.src[1] + off));
-            acc = op1<T, OP>(x0, x1);
-        } else {
-            acc = nt_load((const Item *) (a.src[0] + off));
-            for (int j = 1; j < a.nsrc; ++j) acc = op1<T, OP>(acc, nt_load((const Item *) (a.src[j] + off)));
-        }
-        nt_store((Item *) (a.dst + off), acc);
-    }
-    if (VEC && blockIdx.x == 0) {
-        const int tid = threadIdx.x;
-        const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
-        for (int pass = 0; pass < 2; ++pass) {
-            if ((uint64_t) tid >= (pass == 0 ? a.head : a.tail)) continue;
-            const uint64_t e = pass == 0 ? (uint64_t) tid : tail_off + tid;
-            T acc = ((const T *) a.src[0])[e];
-            for (int j = 1; j < a.nsrc; ++j) acc = op1<T, OP>(acc, ((const T *) a.src[j])[e]);
-            ((T *) a.dst)[e] = acc;
-        }
-    }
-}
-
-// Standalone team barrier (ishmem_team_sync / barrier_all analogue): one workgroup.
-__global__ __launch_bounds__(kBlock) void team_sync_kernel(ReduceArgs a)
-{
-    const bool ok = pe_barrier(a, kPhaseSync, 0);
-    if (threadIdx.x == 0 && a.ret) *a.ret = ok ? 0 : 1;
-}
-
-// Canonical kernel type: MIN/MAX keep the signedness, every other integer op folds on the
-// unsigned type of the same width (bit-identical two's-complement results).
-template <int OP, typename S, typename U>
-using Canon = std::conditional_t<(OP == ISHMEMI_OP_MAX || OP == ISHMEMI_OP_MIN), S, U>;
-
-template <typename T, int OP>
-hipError_t ar_t(bool vec, const ReduceArgs &a, int grid, hipStream_t s)
-{
-    if (vec) hipLaunchKernelGGL((allreduce_kernel<T, OP, true>), dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((allreduce_kernel<T, OP, false>), dim3(grid), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
-}
-
-template <typename T, int OP, bool VEC>
-void fi_ns(const FaninArgs &a, int grid, hipStream_t s)
-{
-    if (a.nsrc == 1) hipLaunchKernelGGL((fanin_kernel<T, OP, VEC, 1>), dim3(grid), dim3(kFaninBlock), 0, s, a);
-    else if (a.nsrc == 2) hipLaunchKernelGGL((fanin_kernel<T, OP, VEC, 2>), dim3(grid), dim3(kFaninBlock), 0, s, a);
-    else hipLaunchKernelGGL((fanin_kernel<T, OP, VEC, 0>), dim3(grid), dim3(kFaninBlock), 0, s, a);
-}
-
-template <typename T, int OP>
-hipError_t fi_t(bool vec, const FaninArgs &a, int grid, hipStream_t s)
-{
-    if (vec) fi_ns<T, OP, true>(a, grid, s);
-    else fi_ns<T, OP, false>(a, grid, s);
-    return hipGetLastError();
-}
-
-template <int OP, typename A, typename L>
-hipError_t dispatch_dt(int dt, L &&launch)
-{
-    constexpr bool fp_ok = OP >= ISHMEMI_OP_MAX;
-    switch (dt) {
-        case ISHMEMI_DT_INT8: return launch.template operator()<Canon<OP, int8_t, uint8_t>, OP>();
-        case ISHMEMI_DT_INT16: return launch.template operator()<Canon<OP, int16_t, uint16_t>, OP>();
-        case ISHMEMI_DT_INT32: return launch.template operator()<Canon<OP, int32_t, uint32_t>, OP>();
-        case ISHMEMI_DT_INT64: return launch.template operator()<Canon<OP, int64_t, uint64_t>, OP>();
-        case ISHMEMI_DT_UINT8: return launch.template operator()<uint8_t, OP>();
-        case ISHMEMI_DT_UINT16: return launch.template operator()<uint16_t, OP>();
-        case ISHMEMI_DT_UINT32: return launch.template operator()<uint32_t, OP>();
-        case ISHMEMI_DT_UINT64: return launch.template operator()<uint64_t, OP>();
-        case ISHMEMI_DT_FLOAT:
-            if constexpr (fp_ok) return launch.template operator()<float, OP>();
-            else return hipErrorInvalidValue;
-        case ISHMEMI_DT_DOUBLE:
-            if constexpr (fp_ok) return launch.template operator()<double, OP>();
-            else return hipErrorInvalidValue;
-        default: return hipErrorInvalidValue;
-    }
-}
-
-template <typename A, typename L>
-hipError_t dispatch(int op, int dt, L &&launch)
-{
-    switch (op) {
-        case ISHMEMI_OP_AND: return dispatch_dt<ISHMEMI_OP_AND, A>(dt, launch);
-        case ISHMEMI_OP_OR: return dispatch_dt<ISHMEMI_OP_OR, A>(dt, launch);
-        case ISHMEMI_OP_XOR: return dispatch_dt<ISHMEMI_OP_XOR, A>(dt, launch);
-        case ISHMEMI_OP_MAX: return dispatch_dt<ISHMEMI_OP_MAX, A>(dt, launch);
-        case ISHMEMI_OP_MIN: return dispatch_dt<ISHMEMI_OP_MIN, A>(dt, launch);
-        case ISHMEMI_OP_SUM: return dispatch_dt<ISHMEMI_OP_SUM, A>(dt, launch);
-        case ISHMEMI_OP_PROD: return dispatch_dt<ISHMEMI_OP_PROD, A>(dt, launch);
-        default: return hipErrorInvalidValue;
-    }
-}
-
-}  // namespace
+#define ISHMEMI_DECL_OP(N)                                                                         \
+    hipError_t launch_allreduce_op##N(int dt, bool vec, const ReduceArgs &a, int grid,             \
+                                      hipStream_t s);                                              \
+    hipError_t launch_fanin_op##N(int dt, bool vec, const FaninArgs &a, int grid, hipStream_t s);
+ISHMEMI_DECL_OP(0)
+ISHMEMI_DECL_OP(1)
+ISHMEMI_DECL_OP(2)
+ISHMEMI_DECL_OP(3)
+ISHMEMI_DECL_OP(4)
+ISHMEMI_DECL_OP(5)
+ISHMEMI_DECL_OP(6)
 
 hipError_t launch_allreduce(int op, int dt, bool vec, const ReduceArgs &a, int grid, hipStream_t s)
 {
     if (!op_dtype_valid(op, dt)) return hipErrorInvalidValue;
-    auto l = [&]<typename T, int OP>() { return ar_t<T, OP>(vec, a, grid, s); };
-    return dispatch<ReduceArgs>(op, dt, l);
+    switch (op) {
+        case 0: return launch_allreduce_op0(dt, vec, a, grid, s);
+        case 1: return launch_allreduce_op1(dt, vec, a, grid, s);
+        case 2: return launch_allreduce_op2(dt, vec, a, grid, s);
+        case 3: return launch_allreduce_op3(dt, vec, a, grid, s);
+        case 4: return launch_allreduce_op4(dt, vec, a, grid, s);
+        case 5: return launch_allreduce_op5(dt, vec, a, grid, s);
+        case 6: return launch_allreduce_op6(dt, vec, a, grid, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_fanin(int op, int dt, bool vec, const FaninArgs &a, int grid, hipStream_t s)
 {
     if (!op_dtype_valid(op, dt)) return hipErrorInvalidValue;
-    auto l = [&]<typename T, int OP>() { return fi_t<T, OP>(vec, a, grid, s); };
-    return dispatch<FaninArgs>(op, dt, l);
+    switch (op) {
+        case 0: return launch_fanin_op0(dt, vec, a, grid, s);
+        case 1: return launch_fanin_op1(dt, vec, a, grid, s);
+        case 2: return launch_fanin_op2(dt, vec, a, grid, s);
+        case 3: return launch_fanin_op3(dt, vec, a, grid, s);
+        case 4: return launch_fanin_op4(dt, vec, a, grid, s);
+        case 5: return launch_fanin_op5(dt, vec, a, grid, s);
+        case 6: return launch_fanin_op6(dt, vec, a, grid, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_team_sync(const ReduceArgs &a, hipStream_t s)

@@ -1,0 +1,27 @@
+// ishmem_amd — instantiation unit for ONE reduction op (compiled once per op with
+// -DISHMEMI_KOP=<0..6>, see ishmem_amd/_build.py): all element types of that op, both kernels.
+#include "kernels_impl.h"
+
+#ifndef ISHMEMI_KOP
+#error "compile with -DISHMEMI_KOP=<op>"
+#endif
+#define ISHMEMI_CAT2(a, b) a##b
+#define ISHMEMI_CAT(a, b) ISHMEMI_CAT2(a, b)
+
+namespace ishmemi {
+
+hipError_t ISHMEMI_CAT(launch_allreduce_op, ISHMEMI_KOP)(int dt, bool vec, const ReduceArgs &a,
+                                                         int grid, hipStream_t s)
+{
+    auto l = [&]<typename T, int OP>() { return ar_t<T, OP>(vec, a, grid, s); };
+    return dispatch_dt<ISHMEMI_KOP, ReduceArgs>(dt, l);
+}
+
+hipError_t ISHMEMI_CAT(launch_fanin_op, ISHMEMI_KOP)(int dt, bool vec, const FaninArgs &a, int grid,
+                                                     hipStream_t s)
+{
+    auto l = [&]<typename T, int OP>() { return fi_t<T, OP>(vec, a, grid, s); };
+    return dispatch_dt<ISHMEMI_KOP, FaninArgs>(dt, l);
+}
+
+}  // namespace ishmemi
