@@ -118,6 +118,7 @@ __device__ __forceinline__ I cload(__amdgpu_buffer_rsrc_t r, uint32_t off)
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // Streaming store that does not keep the line in L2 / Infinity Cache (output is not re-read).
 template <typename I>
@@ -125,6 +126,18 @@ __device__ __forceinline__ void nt_store(I *p, const I &v)
 {
     if constexpr (sizeof(I) == 16) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (u32x4 *) p);
     else __builtin_nontemporal_store(v, p);
+}
+
+// System-coherent write-through store (sc0 sc1): the line is not left dirty in this XCD's L2, so
+// the release before the hand-off flag is cheap and peers' coherent loads see memory.
+template <typename I>
+__device__ __forceinline__ void wt_store(__amdgpu_buffer_rsrc_t r, uint32_t off, const I &v)
+{
+    if constexpr (sizeof(I) == 16) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, kSysCoherent);
+    else if constexpr (sizeof(I) == 8) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, kSysCoherent);
+    else if constexpr (sizeof(I) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, kSysCoherent);
+    else if constexpr (sizeof(I) == 2) __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, v), r, off, 0, kSysCoherent);
+    else __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, v), r, off, 0, kSysCoherent);
 }
 
 __device__ __forceinline__ uint32_t *flag_slot(uint32_t *base, int phase, int block)
@@ -138,6 +151,7 @@ __device__ __forceinline__ uint32_t *flag_slot(uint32_t *base, int phase, int bl
 // its own slot of every peer's flag row, then polls its local row until every peer's slot
 // holds the epoch (wrap-safe compare).  Called by ALL threads of the block; returns false on
 // timeout (recorded in *err) so the caller can drain instead of hanging the GPU.
+template <bool RELEASE>
 __device__ bool pe_barrier(const ReduceArgs &a, int phase, int block)
 {
     __shared__ int s_ok;
@@ -147,11 +161,16 @@ __device__ bool pe_barrier(const ReduceArgs &a, int phase, int block)
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         const int p = a.p, me = a.me;
-        // System-scope release: write back this XCD's L2 so the bytes this workgroup wrote are
-        // visible to peers' coherent loads.  The asm wait guards against the compiler dropping
-        // the wait after buffer_wbl2 (MI355X_MICROARCH.md, compiler hazard).
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (RELEASE) {
+            // Only the mid barrier hands off bytes this launch wrote (the reduced chunk).  Those
+            // are stored system-coherent write-through (wt_store), so this system-scope release
+            // has no dirty lines of ours to write back; it orders them before the flag.  The asm
+            // wait guards against the compiler dropping the wait after buffer_wbl2
+            // (MI355X_MICROARCH.md, compiler hazard).  Start / end barriers hand off nothing
+            // written in this launch (sources were written back at the producer kernels' end).
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         if (lane == 0) {
             for (int j = 0; j < p; ++j) {
                 if (j == me) continue;
@@ -175,8 +194,11 @@ __device__ bool pe_barrier(const ReduceArgs &a, int phase, int block)
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        // System-scope acquire: drop this CU's L1 / non-coherent L2 lines before reading peers.
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        // No acquire instruction: every load of bytes another PE produced is a system-coherent
+        // (sc0 sc1) load, which neither L1 nor a non-coherent L2 line can satisfy; the wavefront
+        // fence only keeps the compiler from hoisting those loads above the poll
+        // (cdna_hip_programming.md Guideline 16).
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane == 0) {
             s_ok = !timed_out;
             if (timed_out)
@@ -222,14 +244,14 @@ __device__ __forceinline__ void rs_tile(const ReduceArgs &a, uint64_t t0, uint64
                 }
             }
         }
-        Item *dp = (Item *) (a.dst + head_bytes + t0 * IB);
+        const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + head_bytes + t0 * IB));
 #pragma unroll
         for (int u = 0; u < H; ++u) {
             Item acc = x[u][(P - R) % P];  // member 0
 #pragma unroll
             for (int j = 1; j < P; ++j) acc = op1<T, OP>(acc, x[u][(j - R + P) % P]);
             const uint64_t e = (uint64_t) (h * H + u) * kBlock + tid;
-            if (t0 + e < ce) dp[e] = acc;
+            if (t0 + e < ce) wt_store(dr, (uint32_t) (e * IB), acc);
         }
     }
 }
@@ -260,7 +282,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
     const uint64_t G = gridDim.x;
     const int p = a.p, me = a.me;
     const uint64_t head_bytes = VEC ? a.head * sizeof(T) : 0;
-    bool ok = pe_barrier(a, kPhaseStart, b);
+    bool ok = pe_barrier<false>(a, kPhaseStart, b);
 
     // ---- reduce-scatter: fold chunk `me` of every member's source, canonical team order ----
     // The LOAD order is rotated by workgroup index (rot = b mod p), so at any instant the
@@ -307,34 +329,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
                         for (int u = 0; u < kUnroll; ++u) acc[u] = op1<T, OP>(acc[u], x[u]);
                     }
                 }
-                Item *dp = (Item *) (a.dst + head_bytes + t0 * IB);
+                const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + head_bytes + t0 * IB));
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u) {
                     const uint64_t e = (uint64_t) u * kBlock + tid;
-                    if (t0 + e < ce) dp[e] = acc[u];
+                    if (t0 + e < ce) wt_store(dr, (uint32_t) (e * IB), acc[u]);
                 }
             }
         }
         // Unaligned head (owned by member 0) and tail (owned by member p-1), element-wise.
         if (VEC && b == 0) {
             const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
+            // For p >= 2 a member owns at most one of the two regions, so the region base is
+            // wave-uniform; descriptors are based at the region (offsets < 16 B), never at the
+            // array start (a > 2 GiB array would exceed the descriptor's range).
+            const uint64_t rbase = (me == 0 ? 0 : tail_off) * sizeof(T);
             const bool do_head = (me == 0) && ((uint64_t) tid < a.head);
             const bool do_tail = (me == p - 1) && ((uint64_t) tid < a.tail);
             if (do_head || do_tail) {
-                const uint64_t e = do_head ? (uint64_t) tid : tail_off + tid;
+                const uint32_t off = (uint32_t) (tid * sizeof(T));
                 T acc = T();
                 for (int j = 0; j < p; ++j) {
                     T x;
-                    if (j == me) x = ((const T *) a.src[j])[e];
-                    else x = cload<T>(make_rsrc(uniform_ptr(a.src[j])), (uint32_t) (e * sizeof(T)));
+                    if (j == me) x = ((const T *) (a.src[j] + rbase))[tid];
+                    else x = cload<T>(make_rsrc(uniform_ptr(a.src[j] + rbase)), off);
                     acc = (j == 0) ? x : op1<T, OP>(acc, x);
                 }
-                ((T *) a.dst)[e] = acc;
+                wt_store(make_rsrc(uniform_ptr(a.dst + rbase)), off, acc);
             }
         }
     }
 
-    ok = ok && pe_barrier(a, kPhaseMid, b);
+    ok = ok && pe_barrier<true>(a, kPhaseMid, b);
 
     // ---- all-gather: pull every other member's reduced chunk from its dest ----
     if (ok) {
@@ -364,19 +390,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
             }
             if (VEC && b == 0) {
                 const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
+                const uint64_t rbase = (j == 0 ? 0 : tail_off) * sizeof(T);
                 const bool do_head = (j == 0) && ((uint64_t) tid < a.head);
                 const bool do_tail = (j == p - 1) && ((uint64_t) tid < a.tail);
-                if (do_head || do_tail) {
-                    const uint64_t e = do_head ? (uint64_t) tid : tail_off + tid;
-                    ((T *) a.dst)[e] =
-                        cload<T>(make_rsrc(uniform_ptr(a.dstp[j])), (uint32_t) (e * sizeof(T)));
-                }
+                if (do_head || do_tail)
+                    ((T *) (a.dst + rbase))[tid] =
+                        cload<T>(make_rsrc(uniform_ptr(a.dstp[j] + rbase)), (uint32_t) (tid * sizeof(T)));
             }
         }
     }
 
     // ---- end: peers have finished pulling from my dest before anyone returns ----
-    ok = ok && pe_barrier(a, kPhaseEnd, b);
+    ok = ok && pe_barrier<false>(a, kPhaseEnd, b);
     if (b == 0 && tid == 0 && a.ret) *a.ret = ok ? 0 : 1;
 }
 
@@ -433,7 +458,7 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
 // Standalone team barrier (ishmem_team_sync / barrier_all analogue): one workgroup.
 __global__ __launch_bounds__(kBlock) void team_sync_kernel(ReduceArgs a)
 {
-    const bool ok = pe_barrier(a, kPhaseSync, 0);
+    const bool ok = pe_barrier<false>(a, kPhaseSync, 0);
     if (threadIdx.x == 0 && a.ret) *a.ret = ok ? 0 : 1;
 }
 

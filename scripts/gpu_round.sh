@@ -39,6 +39,9 @@ for s in $STEPS; do
     local4) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-128} run bench_local4 600 python -m torch.distributed.run \
                 --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 4 \
                 --steps 10 --warmup 3 --mib ${MIB:-512} ;;
+    sweep1) run sweep1 300 python tools/sweep.py --max-mib 1024 ;;
+    sweep2) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-256} run sweep2 600 python -m torch.distributed.run \
+                --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 tools/sweep.py --max-mib 256 ;;
     prof)   cd /tmp && export TMPDIR=/tmp
             run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                 python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline

@@ -220,6 +220,30 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             ish.ishmem_free(d)
             ish.ishmem_free(s)
 
+        if "huge" in scenarios:
+            # > 2 GiB per PE with a misaligned start and an odd length: the head, the tail and the
+            # 2 GiB descriptor-range boundary are all exercised.  x_pe[i] = (i mod 1024) + pe, so
+            # the exact sum is known in closed form.
+            n = (1 << 29) + (1 << 27) + 5  # 2.5 GiB + 20 B of float32
+            s_base = ish.ishmem_malloc(n * 4 + 64)
+            d_base = ish.ishmem_malloc(n * 4 + 64)
+            s, d = s_base + 4, d_base + 4
+            x = (np.arange(n, dtype=np.int64) % 1024).astype(np.float32) + np.float32(pe)
+            hip.upload(s, x)
+            del x
+            r = ish.ishmem_float_sum_reduce(d, s, n)
+            if r:
+                fails.append(f"pe{pe} huge rc={r} {ish.last_error()}")
+            else:
+                for lo in (0, (1 << 29) - 7, n - 40):
+                    got = hip.download(d + lo * 4, 40, np.float32)
+                    i = np.arange(lo, lo + 40)
+                    exp = (i % 1024).astype(np.float32) * npes + np.float32(npes * (npes - 1) / 2)
+                    if not np.array_equal(got, exp):
+                        fails.append(f"pe{pe} huge: wrong values near element {lo}")
+            ish.ishmem_free(d_base)
+            ish.ishmem_free(s_base)
+
         if ish.lib().ishmemi_c_error_count() != 0:
             fails.append(f"pe{pe} device barrier timeouts: {ish.lib().ishmemi_c_error_count()}")
         ish.ishmem_barrier_all()

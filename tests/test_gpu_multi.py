@@ -56,3 +56,7 @@ def test_stream_staged_team():
 
 def test_large_f32_sum_256MiB_per_pe():
     run_pes(2, ["large"], env={"ISHMEM_MAX_BLOCKS": 64})
+
+
+def test_huge_2p5GiB_per_pe_head_tail_and_2GiB_boundary():
+    run_pes(2, ["huge"], env={"ISHMEM_MAX_BLOCKS": 64, "ISHMEM_SYMMETRIC_SIZE": "6G"}, timeout=400)

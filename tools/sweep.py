@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Size sweep of the reduce path (dev tool): f32 sum (or --op/--dtype) over TEAM_WORLD for sizes
+4 B .. --max-mib, one process per PE (launch with torch.distributed.run for N>1; set
+ISHMEM_BENCH_SAME_DEVICE=1 to put every PE on device 0).  Prints one CSV row per size on rank 0:
+bytes, us per call (max over ranks), algbw GiB/s.  Results are checked against the closed form."""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import uuid
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--max-mib", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    key = f"sw{uuid.uuid4().hex[:10]}"
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        obj = [key]
+        dist.broadcast_object_list(obj, src=0)
+        key = obj[0]
+    import ishmem_amd as ish
+    from ishmem_amd import hip
+    dev = 0 if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else local
+    ish.init(rank, world, dev, key)
+    nmax = (args.max_mib << 20) // 4
+    src = ish.ishmem_malloc(nmax * 4)
+    dst = ish.ishmem_malloc(nmax * 4)
+    hip.upload(src, (np.arange(nmax, dtype=np.int64) % 1024).astype(np.float32) + np.float32(rank))
+    st = hip.stream_create()
+    if rank == 0:
+        print(f"# pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'}")
+        print("bytes,us_per_call,algbw_GiBps,ok")
+    n = 1
+    while n <= nmax:
+        for _ in range(3):
+            ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, st)
+        hip.stream_synchronize(st)
+        if dist is not None:
+            dist.barrier()
+        e0, e1 = hip.Event(), hip.Event()
+        iters = args.iters if n < (1 << 24) else max(3, args.iters // 4)
+        e0.record(st)
+        for _ in range(iters):
+            ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, st)
+        e1.record(st)
+        hip.stream_synchronize(st)
+        us = e0.elapsed_ms(e1) * 1000.0 / iters
+        if dist is not None:
+            t = torch.tensor([us], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            us = float(t[0])
+        k = min(n, 64)
+        got = hip.download(dst + (n - k) * 4, k, np.float32)
+        i = np.arange(n - k, n)
+        exp = (i % 1024).astype(np.float32) * world + np.float32(world * (world - 1) / 2)
+        ok = bool(np.array_equal(got, exp))
+        if rank == 0:
+            print(f"{n * 4},{us:.2f},{n * 4 / 2**30 / (us * 1e-6):.2f},{int(ok)}", flush=True)
+        n *= 4
+    ish.ishmem_finalize()
+
+
+if __name__ == "__main__":
+    main()
