@@ -52,6 +52,56 @@ def pmc_traffic(kernel_tag: str, nbytes: int):
     return None
 
 
+def config5_sweep(ish, hip, src, dst, world, rank, dist, stream):
+    """min/max/prod x int32/float64, 4 KiB .. 64 MiB per PE: us per call (max over ranks), algbw."""
+    import torch
+    out = []
+    nbytes_max = 64 << 20
+    for dtn, npd in (("int32", np.int32), ("double", np.float64)):
+        es = np.dtype(npd).itemsize
+        nmax = nbytes_max // es
+        x = (np.arange(nmax, dtype=np.int64) % 1024).astype(npd) + npd(rank)
+        hip.upload(src, x)
+        base = np.arange(nmax, dtype=np.int64) % 1024
+        for op in ("min", "max", "prod"):
+            if op == "min":
+                exp_full = base.astype(npd)
+            elif op == "max":
+                exp_full = (base + world - 1).astype(npd)
+            else:
+                acc = base.astype(npd) if npd is np.float64 else base.astype(np.uint32)
+                for pe in range(1, world):
+                    acc = acc * (base.astype(npd) + npd(pe)) if npd is np.float64 else \
+                        (acc * (base + pe).astype(np.uint32)).astype(np.uint32)
+                exp_full = acc.astype(npd) if npd is np.float64 else acc.view(np.int32)
+            nb = 4096
+            while nb <= nbytes_max:
+                n = nb // es
+                for _ in range(2):
+                    ish.reduce_on_stream(op, dtn, dst, src, n, None, stream)
+                hip.stream_synchronize(stream)
+                dist.barrier()
+                it = 20 if nb < (8 << 20) else 5
+                e0, e1 = hip.Event(), hip.Event()
+                e0.record(stream)
+                for _ in range(it):
+                    if ish.reduce_on_stream(op, dtn, dst, src, n, None, stream) != 0:
+                        raise RuntimeError(ish.last_error())
+                e1.record(stream)
+                hip.stream_synchronize(stream)
+                us = e0.elapsed_ms(e1) * 1000.0 / it
+                t = torch.tensor([us], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                us = float(t[0])
+                k = min(n, 256)
+                got = hip.download(dst + (n - k) * es, k, npd)
+                ok = bool(np.array_equal(got.view(np.uint8), exp_full[n - k:n].view(np.uint8)))
+                out.append({"op": op, "dtype": dtn, "bytes": nb, "us": round(us, 2),
+                            "algbw_GiBps": round(nb / GiB / (us * 1e-6), 2), "checked": ok})
+                nb *= 4
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -61,6 +111,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--nelems", type=int, default=0, help="override: float32 elements per PE")
     ap.add_argument("--rccl", action="store_true",
                     help="N>1: also time RCCL all_reduce on the same payload (comparison only)")
@@ -234,6 +285,12 @@ def main() -> None:
         except Exception as ex:
             extra["rccl_allreduce"] = {"error": str(ex)}
 
+    if world > 1 and not args.no_sweep:
+        # BASELINE configs[4] (min/max/prod x int32/float64 across the PEs), sizes 4 KiB ..
+        # 64 MiB per PE (the 4 GiB end of that sweep is left to tools/sweep.py).  Inputs
+        # x_pe[i] = (i mod 1024) + pe; every result is checked against the canonical fold.
+        extra["config5_sweep"] = config5_sweep(ish, hip, src, dst, world, rank, dist, stream)
+
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         import oracle  # CPU baseline leg only: the reference's host-proxy reduce, restated
@@ -242,6 +299,13 @@ def main() -> None:
         cpu = {"value": B / GiB / t_cpu, "unit": "GiB/s", "cores": 1, "kind": "port",
                "sample": f"full workload: 1 PE f32 sum-reduce of {B / 2**20:g} MiB through 64 KiB host "
                          f"bounce chunks (reduce_impl.h:186-228), best of {reps}"}
+        # BASELINE configs[0]: int32 sum, 2 PEs, host loopback through the proxy path (no GPU):
+        # two processes exchanging 64 KiB bounce chunks over shared memory.
+        n1 = 16 << 20
+        t1 = oracle.host_proxy_time(oracle.OPS["sum"], oracle.DTYPES["int32"], n1, 2, 3)
+        extra["cpu_config1"] = {"value": n1 * 4 / GiB / t1, "unit": "GiB/s", "cores": 2,
+                                "kind": "port", "sample": "int32 sum-reduce, 2 PEs (processes), "
+                                "64 MiB per PE, 64 KiB bounce chunks, best of 3"}
 
     ish.ishmem_free(dst)
     ish.ishmem_free(src)
@@ -266,4 +330,13 @@ def main() -> None:
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as exc:  # always leave one JSON line for the driver, with the reason
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({
+                "metric": "GiB/s device-resident float32 sum-reduce at 1/2/4/8 PEs vs HBM+xGMI roofline",
+                "value": None, "unit": "GiB/s", "n_gpus": int(os.environ.get("WORLD_SIZE", "1")),
+                "higher_is_better": True, "error": f"{type(exc).__name__}: {exc}"}))
+        sys.stdout.flush()
+        raise
