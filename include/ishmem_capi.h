@@ -128,6 +128,31 @@ int ishmemi_c_reduce_on_stream(int team, int op, int dtype, void *dest, const vo
 int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n,
                       void *stream);
 
+/* ---- device-initiated collectives ----------------------------------------------------------
+ * The reference's device-callable reductions (ishmemx_<TN>_<op>_reduce_work_group,
+ * src/collectives/reduce_impl.h:386-418, :505-518, src/ishmemx.h:1648-1699) read the library
+ * state from a SYCL device global.  A HIP user kernel lives in its own code object, so the state
+ * is handed to it explicitly: ishmemi_c_device_ctx() returns a DEVICE pointer to this struct,
+ * which the user passes to its kernel and on to the header-only device API (ishmemx_device.h).
+ * Layout is part of the ABI. */
+#define ISHMEMI_C_MAX_PES 16
+#define ISHMEMI_C_MAX_TEAMS 16
+#define ISHMEMI_C_DEV_PHASES 4
+typedef struct {
+    int32_t pe, npes;
+    uint64_t timeout_ticks;                       /* s_memrealtime ticks (100 MHz) */
+    char *heap_base;                              /* this PE's symmetric heap */
+    uint64_t heap_size;
+    char *peer_heap[ISHMEMI_C_MAX_PES];           /* every PE's heap, mapped here */
+    uint32_t *my_dflags;                          /* [team][phase][pe] epochs, fine-grained */
+    uint32_t *peer_dflags[ISHMEMI_C_MAX_PES];
+    uint32_t *epochs;                             /* [team] last device-API epoch (this PE) */
+    uint32_t *err;                                /* device-API error word (host-visible) */
+    int32_t team_start[ISHMEMI_C_MAX_TEAMS], team_stride[ISHMEMI_C_MAX_TEAMS];
+    int32_t team_size[ISHMEMI_C_MAX_TEAMS], team_my_idx[ISHMEMI_C_MAX_TEAMS];
+} ishmemi_c_device_ctx_t;
+void *ishmemi_c_device_ctx(void);
+
 /* ---- diagnostics / parameters ----------------------------------------------------------------
  * ishmemi_c_set_param names: "max_blocks" (workgroups per collective launch, <= 1024),
  * "timeout_ms" (bound on every device-side spin), "debug". */

@@ -1,0 +1,241 @@
+/* ishmem_amd — device-callable (work-group) reductions, header-only HIP.
+ *
+ * Analogue of the reference's
+ *   template <typename Group> int ishmemx_<TYPENAME>_<op>_reduce_work_group([team,] TYPE *dest,
+ *                                  const TYPE *source, size_t nreduce, const Group &grp)
+ * (src/ishmemx.h:1648-1699, src/collectives/reduce_impl.h:386-418, :505-518): called by EVERY
+ * thread of ONE work-group on every PE of the team, from inside a user kernel.  The library state
+ * is passed explicitly (`ctx` = ishmemi_c_device_ctx(), handed to the kernel as an argument),
+ * because a HIP user kernel cannot see the library's device globals the way SYCL's do.
+ *
+ *   __global__ void k(const ishmemi_c_device_ctx_t *ctx, float *dst, const float *src, size_t n) {
+ *       ... produce src ...
+ *       int rc = ishmemx_float_sum_reduce_work_group(ctx, dst, src, n);
+ *   }
+ *
+ * Algorithm: the same direct reduce-scatter + all-gather as the host-launched kernel, executed by
+ * the calling work-group (member c folds chunk c of every member's source in canonical team order
+ * with system-coherent loads, stores it write-through, team barrier, then pulls the other chunks).
+ * `source` must have been written by the calling work-group or by earlier kernels (the start
+ * barrier releases this work-group's own writes).  Returns 0, or nonzero if a peer did not arrive
+ * within the library's timeout.  dest/source must be symmetric-heap addresses.
+ */
+#ifndef ISHMEM_AMD_ISHMEMX_DEVICE_H
+#define ISHMEM_AMD_ISHMEMX_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "ishmem_capi.h"
+
+namespace ishmemx_dev {
+
+template <typename T, int OP>
+__device__ __forceinline__ T op1(T a, T b)
+{
+    using W = std::conditional_t<(sizeof(T) == 8), uint64_t, uint32_t>;
+    if constexpr (OP == ISHMEMI_OP_AND) return (T) (a & b);
+    else if constexpr (OP == ISHMEMI_OP_OR) return (T) (a | b);
+    else if constexpr (OP == ISHMEMI_OP_XOR) return (T) (a ^ b);
+    else if constexpr (OP == ISHMEMI_OP_MAX) {
+        if constexpr (std::is_floating_point_v<T>) return fmax(a, b);
+        else return (a < b) ? b : a;
+    } else if constexpr (OP == ISHMEMI_OP_MIN) {
+        if constexpr (std::is_floating_point_v<T>) return fmin(a, b);
+        else return (b < a) ? b : a;
+    } else if constexpr (OP == ISHMEMI_OP_SUM) {
+        if constexpr (std::is_floating_point_v<T>) return a + b;
+        else return (T) (std::make_unsigned_t<T>) ((W) (std::make_unsigned_t<T>) a + (W) (std::make_unsigned_t<T>) b);
+    } else {
+        if constexpr (std::is_floating_point_v<T>) return a * b;
+        else return (T) (std::make_unsigned_t<T>) ((W) (std::make_unsigned_t<T>) a * (W) (std::make_unsigned_t<T>) b);
+    }
+}
+
+// System-coherent element access (sc0 sc1): bypasses L1 / non-coherent L2 copies.
+template <typename T>
+__device__ __forceinline__ T sys_load(const T *p)
+{
+    using U = std::conditional_t<sizeof(T) == 8, uint64_t, std::conditional_t<sizeof(T) == 4, uint32_t,
+              std::conditional_t<sizeof(T) == 2, uint16_t, uint8_t>>>;
+    const U v = __hip_atomic_load((const U *) p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return __builtin_bit_cast(T, v);
+}
+
+template <typename T>
+__device__ __forceinline__ void sys_store(T *p, T x)
+{
+    using U = std::conditional_t<sizeof(T) == 8, uint64_t, std::conditional_t<sizeof(T) == 4, uint32_t,
+              std::conditional_t<sizeof(T) == 2, uint16_t, uint8_t>>>;
+    __hip_atomic_store((U *) p, __builtin_bit_cast(U, x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ char *peer_addr(const ishmemi_c_device_ctx_t *c, const void *p, int pe)
+{
+    return c->peer_heap[pe] + ((const char *) p - c->heap_base);
+}
+
+// Team barrier among the calling work-groups (one per member): thread 0 stores the epoch into
+// its slot of every peer's row and polls its own row; bounded by the library timeout.
+__device__ inline bool wg_barrier(const ishmemi_c_device_ctx_t *c, int team, int phase,
+                                  uint32_t epoch, bool release)
+{
+    __shared__ int s_ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x + threadIdx.y + threadIdx.z == 0) {
+        const int size = c->team_size[team], me = c->team_my_idx[team];
+        const size_t row = ((size_t) team * ISHMEMI_C_DEV_PHASES + phase) * ISHMEMI_C_MAX_PES;
+        if (release) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        for (int j = 0; j < size; ++j) {
+            if (j == me) continue;
+            const int gpe = c->team_start[team] + j * c->team_stride[team];
+            __hip_atomic_store(c->peer_dflags[gpe] + row + me, epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        bool ok = true;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (int j = 0; j < size && ok; ++j) {
+            if (j == me) continue;
+            while ((int32_t) (__hip_atomic_load(c->my_dflags + row + j, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > c->timeout_ticks) {
+                    ok = false;
+                    __hip_atomic_fetch_or(c->err, 1u << phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+template <typename T, int OP>
+__device__ int reduce_work_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, const T *source,
+                                 size_t nreduce)
+{
+    __shared__ uint32_t s_epoch;
+    const int tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
+    const int nthr = blockDim.x * blockDim.y * blockDim.z;
+    const int size = c->team_size[team], me = c->team_my_idx[team];
+    if (size <= 0 || me < 0) return 1;
+    if (tid == 0)
+        s_epoch = __hip_atomic_fetch_add(c->epochs + team, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __syncthreads();
+    const uint32_t epoch = s_epoch;
+    if (size == 1) {  // one PE: dest = source (reduce_impl.h:288-289)
+        if (dest != source)
+            for (size_t i = tid; i < nreduce; i += nthr) dest[i] = source[i];
+        __syncthreads();
+        return 0;
+    }
+    // Start: every member's source is complete (this work-group's own writes released).
+    if (!wg_barrier(c, team, 0, epoch, true)) return 1;
+    const size_t per = ((nreduce + size - 1) / size + 63) & ~(size_t) 63;
+    const size_t cs = (size_t) me * per < nreduce ? (size_t) me * per : nreduce;
+    const size_t ce = cs + per < nreduce ? cs + per : nreduce;
+    const int start = c->team_start[team], stride = c->team_stride[team];
+    for (size_t i = cs + tid; i < ce; i += nthr) {
+        T acc = T();
+        for (int j = 0; j < size; ++j) {
+            const int gpe = start + j * stride;
+            const T x = (j == me) ? source[i] : sys_load((const T *) peer_addr(c, source + i, gpe));
+            acc = (j == 0) ? x : op1<T, OP>(acc, x);
+        }
+        sys_store(dest + i, acc);  // write-through: peers pull it after the next barrier
+    }
+    if (!wg_barrier(c, team, 1, epoch, true)) return 1;
+    for (int k = 1; k < size; ++k) {
+        const int j = (me + k) % size;
+        const int gpe = start + j * stride;
+        const size_t js = (size_t) j * per < nreduce ? (size_t) j * per : nreduce;
+        const size_t je = js + per < nreduce ? js + per : nreduce;
+        for (size_t i = js + tid; i < je; i += nthr) dest[i] = sys_load((const T *) peer_addr(c, dest + i, gpe));
+    }
+    // End: no member returns while a peer may still read its dest.
+    return wg_barrier(c, team, 2, epoch, false) ? 0 : 1;
+}
+
+template <typename T>
+constexpr bool is_canon()
+{
+    return std::is_arithmetic_v<T> && sizeof(T) <= 8;
+}
+
+}  // namespace ishmemx_dev
+
+#define ISHMEMX_DEV_GENERIC(OPNAME, OPC)                                                           \
+    template <typename T>                                                                          \
+    __device__ inline int ishmemx_##OPNAME##_reduce_work_group(                                    \
+        const ishmemi_c_device_ctx_t *ctx, T *dest, const T *source, size_t nreduce)               \
+    {                                                                                              \
+        return ishmemx_dev::reduce_work_group<T, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,     \
+                                                      nreduce);                                    \
+    }                                                                                              \
+    template <typename T>                                                                          \
+    __device__ inline int ishmemx_##OPNAME##_reduce_work_group(                                    \
+        const ishmemi_c_device_ctx_t *ctx, int team, T *dest, const T *source, size_t nreduce)     \
+    {                                                                                              \
+        return ishmemx_dev::reduce_work_group<T, OPC>(ctx, team, dest, source, nreduce);           \
+    }
+
+ISHMEMX_DEV_GENERIC(and, ISHMEMI_OP_AND)
+ISHMEMX_DEV_GENERIC(or, ISHMEMI_OP_OR)
+ISHMEMX_DEV_GENERIC(xor, ISHMEMI_OP_XOR)
+ISHMEMX_DEV_GENERIC(max, ISHMEMI_OP_MAX)
+ISHMEMX_DEV_GENERIC(min, ISHMEMI_OP_MIN)
+ISHMEMX_DEV_GENERIC(sum, ISHMEMI_OP_SUM)
+ISHMEMX_DEV_GENERIC(prod, ISHMEMI_OP_PROD)
+
+#define ISHMEMX_DEV_TYPED(TYPENAME, TYPE, OPNAME, OPC)                                              \
+    __device__ inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_work_group(                       \
+        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nreduce)         \
+    {                                                                                              \
+        return ishmemx_dev::reduce_work_group<TYPE, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,  \
+                                                         nreduce);                                 \
+    }                                                                                              \
+    __device__ inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_work_group(                       \
+        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source,               \
+        size_t nreduce)                                                                            \
+    {                                                                                              \
+        return ishmemx_dev::reduce_work_group<TYPE, OPC>(ctx, team, dest, source, nreduce);        \
+    }
+
+/* Same TYPENAME x op matrix as the host API (src/collectives/reduce.cpp:95-417). */
+#define ISHMEMX_DEV_BITWISE_TYPES(X, OPNAME, OPC)                                                   \
+    X(uchar, unsigned char, OPNAME, OPC) X(ushort, unsigned short, OPNAME, OPC)                    \
+    X(uint, unsigned int, OPNAME, OPC) X(ulong, unsigned long, OPNAME, OPC)                        \
+    X(ulonglong, unsigned long long, OPNAME, OPC) X(int8, int8_t, OPNAME, OPC)                     \
+    X(int16, int16_t, OPNAME, OPC) X(int32, int32_t, OPNAME, OPC) X(int64, int64_t, OPNAME, OPC)   \
+    X(uint8, uint8_t, OPNAME, OPC) X(uint16, uint16_t, OPNAME, OPC)                                \
+    X(uint32, uint32_t, OPNAME, OPC) X(uint64, uint64_t, OPNAME, OPC) X(size, size_t, OPNAME, OPC)
+#define ISHMEMX_DEV_ARITH_TYPES(X, OPNAME, OPC)                                                     \
+    X(char, char, OPNAME, OPC) X(schar, signed char, OPNAME, OPC) X(short, short, OPNAME, OPC)     \
+    X(int, int, OPNAME, OPC) X(long, long, OPNAME, OPC) X(longlong, long long, OPNAME, OPC)        \
+    X(ptrdiff, ptrdiff_t, OPNAME, OPC) X(uchar, unsigned char, OPNAME, OPC)                        \
+    X(ushort, unsigned short, OPNAME, OPC) X(uint, unsigned int, OPNAME, OPC)                      \
+    X(ulong, unsigned long, OPNAME, OPC) X(ulonglong, unsigned long long, OPNAME, OPC)             \
+    X(int8, int8_t, OPNAME, OPC) X(int16, int16_t, OPNAME, OPC) X(int32, int32_t, OPNAME, OPC)     \
+    X(int64, int64_t, OPNAME, OPC) X(uint8, uint8_t, OPNAME, OPC) X(uint16, uint16_t, OPNAME, OPC) \
+    X(uint32, uint32_t, OPNAME, OPC) X(uint64, uint64_t, OPNAME, OPC) X(size, size_t, OPNAME, OPC) \
+    X(float, float, OPNAME, OPC) X(double, double, OPNAME, OPC)
+
+ISHMEMX_DEV_BITWISE_TYPES(ISHMEMX_DEV_TYPED, and, ISHMEMI_OP_AND)
+ISHMEMX_DEV_BITWISE_TYPES(ISHMEMX_DEV_TYPED, or, ISHMEMI_OP_OR)
+ISHMEMX_DEV_BITWISE_TYPES(ISHMEMX_DEV_TYPED, xor, ISHMEMI_OP_XOR)
+ISHMEMX_DEV_ARITH_TYPES(ISHMEMX_DEV_TYPED, max, ISHMEMI_OP_MAX)
+ISHMEMX_DEV_ARITH_TYPES(ISHMEMX_DEV_TYPED, min, ISHMEMI_OP_MIN)
+ISHMEMX_DEV_ARITH_TYPES(ISHMEMX_DEV_TYPED, sum, ISHMEMI_OP_SUM)
+ISHMEMX_DEV_ARITH_TYPES(ISHMEMX_DEV_TYPED, prod, ISHMEMI_OP_PROD)
+
+#endif /* ISHMEM_AMD_ISHMEMX_DEVICE_H */

@@ -24,7 +24,12 @@
 namespace ishmemi {
 namespace {
 
-constexpr int kMaxTeams = 16;
+constexpr int kMaxTeams = ISHMEMI_C_MAX_TEAMS;
+static_assert(kMaxPes == ISHMEMI_C_MAX_PES, "device ctx layout");
+// Device-API flags ([team][phase][pe] u32) follow the host-launch flag blocks in the same
+// fine-grained, IPC-shared allocation.
+constexpr size_t kDevFlagWordsPerTeam = (size_t) ISHMEMI_C_DEV_PHASES * kMaxPes;
+constexpr size_t kDevFlagBytes = (size_t) kMaxTeams * kDevFlagWordsPerTeam * 4;
 constexpr size_t kHeapAlign = 256;
 
 thread_local std::string g_last_error;
@@ -99,8 +104,10 @@ struct State {
     uint32_t *flags = nullptr;  // kMaxTeams flag blocks, fine-grained device memory
     bool flags_fine_grained = false;
     uint32_t *peer_flags[kMaxPes] = {};
-    uint32_t *err_host = nullptr;  // host-mapped error words, one per team
+    uint32_t *err_host = nullptr;  // host-mapped error words, one per team (+1: device API)
     uint32_t *err_dev = nullptr;
+    ishmemi_c_device_ctx_t *dctx = nullptr;  // device copy of the device-API context
+    uint32_t *dev_epochs = nullptr;
 
     char *staging = nullptr;  // symmetric staging region for non-heap / host buffers
     size_t staging_bytes = 0;
@@ -428,6 +435,39 @@ int reduce_impl(int team, int op, int dt, void *dst, const void *src, size_t n, 
     return 0;
 }
 
+uint32_t *dev_flags(uint32_t *flags_base)
+{
+    return flags_base ? flags_base + (size_t) kMaxTeams * (kTeamFlagBytes / 4) : nullptr;
+}
+
+// Refresh the device copy of the device-API context (after init and after team changes).
+int sync_device_ctx(State &s)
+{
+    ishmemi_c_device_ctx_t c;
+    memset(&c, 0, sizeof(c));
+    c.pe = s.pe;
+    c.npes = s.npes;
+    c.timeout_ticks = (uint64_t) s.timeout_ms * 100000ull;
+    c.heap_base = s.heap;
+    c.heap_size = s.heap_size;
+    for (int j = 0; j < s.npes; ++j) {
+        c.peer_heap[j] = s.peer_heap[j];
+        c.peer_dflags[j] = dev_flags(s.peer_flags[j]);
+    }
+    c.my_dflags = dev_flags(s.flags);
+    c.epochs = s.dev_epochs;
+    c.err = s.err_dev + kMaxTeams;
+    for (int t = 0; t < kMaxTeams; ++t) {
+        const Team &tm = s.teams[t];
+        c.team_start[t] = tm.start;
+        c.team_stride[t] = tm.stride;
+        c.team_size[t] = tm.valid ? tm.size : 0;
+        c.team_my_idx[t] = tm.valid ? tm.my_idx : -1;
+    }
+    HIP_TRY(hipMemcpy(s.dctx, &c, sizeof(c), hipMemcpyHostToDevice));
+    return 0;
+}
+
 int init_impl(int pe, int npes, int device, const std::string &key)
 {
     State &s = S();
@@ -456,7 +496,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.free_list[0] = s.heap_size;
 
     // Barrier flags: fine-grained (uncached) device memory, written by peers over xGMI.
-    const size_t flag_bytes = (size_t) kMaxTeams * kTeamFlagBytes;
+    const size_t flag_bytes = (size_t) kMaxTeams * kTeamFlagBytes + kDevFlagBytes;
     if (hipExtMallocWithFlags((void **) &s.flags, flag_bytes, hipDeviceMallocUncached) == hipSuccess) {
         s.flags_fine_grained = true;
     } else {
@@ -465,9 +505,9 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         s.flags_fine_grained = false;
     }
     HIP_TRY(hipMemset(s.flags, 0, flag_bytes));
-    HIP_TRY(hipHostMalloc((void **) &s.err_host, kMaxTeams * sizeof(uint32_t),
+    HIP_TRY(hipHostMalloc((void **) &s.err_host, (kMaxTeams + 1) * sizeof(uint32_t),
                           hipHostMallocMapped | hipHostMallocCoherent));
-    memset(s.err_host, 0, kMaxTeams * sizeof(uint32_t));
+    memset(s.err_host, 0, (kMaxTeams + 1) * sizeof(uint32_t));
     HIP_TRY(hipHostGetDevicePointer((void **) &s.err_dev, s.err_host, 0));
     HIP_TRY(hipDeviceSynchronize());
 
@@ -541,6 +581,10 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.staging_bytes = parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20);
     s.staging = (char *) heap_alloc(s, s.staging_bytes, kHeapAlign);
     if (!s.staging) return 1;
+    HIP_TRY(hipMalloc((void **) &s.dctx, sizeof(ishmemi_c_device_ctx_t)));
+    HIP_TRY(hipMalloc((void **) &s.dev_epochs, kMaxTeams * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(s.dev_epochs, 0, kMaxTeams * sizeof(uint32_t)));
+    if (sync_device_ctx(s)) return 1;
     s.initialized = true;
     return 0;
 }
@@ -615,6 +659,10 @@ int ishmemi_c_finalize(void)
     hipFree(s.heap);
     hipFree(s.flags);
     hipHostFree(s.err_host);
+    hipFree(s.dctx);
+    hipFree(s.dev_epochs);
+    s.dctx = nullptr;
+    s.dev_epochs = nullptr;
     s.heap = nullptr;
     s.flags = nullptr;
     s.err_host = s.err_dev = nullptr;
@@ -758,8 +806,12 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
         s.teams[slot] = t;
         // Fresh flag block: zero it locally, then the parent sync below orders the zeroing
         // before any member's first barrier on the new team.
-        if (hipMemset(team_flags(s.flags, slot), 0, kTeamFlagBytes) != hipSuccess)
+        if (hipMemset(team_flags(s.flags, slot), 0, kTeamFlagBytes) != hipSuccess ||
+            hipMemset(dev_flags(s.flags) + (size_t) slot * kDevFlagWordsPerTeam, 0,
+                      kDevFlagWordsPerTeam * 4) != hipSuccess ||
+            hipMemset(s.dev_epochs + slot, 0, sizeof(uint32_t)) != hipSuccess)
             return fail("team_split_strided: flag reset failed");
+        if (sync_device_ctx(s)) return 1;
         if (hipDeviceSynchronize() != hipSuccess) return fail("team_split_strided: sync failed");
     }
     if (ishmemi_c_team_sync(parent)) return 1;
@@ -773,6 +825,7 @@ void ishmemi_c_team_destroy(int team)
     std::lock_guard<std::mutex> lk(s.mu);
     if (team <= ISHMEMI_C_TEAM_NODE || team >= kMaxTeams) return;
     s.teams[team] = Team{};
+    sync_device_ctx(s);
 }
 
 int ishmemi_c_team_sync(int team)
@@ -829,6 +882,12 @@ int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int
     return 0;
 }
 
+void *ishmemi_c_device_ctx(void)
+{
+    State &s = S();
+    return s.initialized ? (void *) s.dctx : nullptr;
+}
+
 const char *ishmemi_c_last_error(void) { return g_last_error.c_str(); }
 
 int ishmemi_c_set_param(const char *name, long long value)
@@ -855,7 +914,12 @@ long long ishmemi_c_get_param(const char *name)
     return -1;
 }
 
-int ishmemi_c_error_count(void) { return S().error_count; }
+int ishmemi_c_error_count(void)
+{
+    State &s = S();
+    const int dev = (s.err_host && s.err_host[kMaxTeams]) ? 1 : 0;
+    return s.error_count + dev;
+}
 
 size_t ishmemi_c_dtype_size(int dtype)
 {

@@ -1,0 +1,117 @@
+// Device-initiated reductions through include/ishmemx_device.h, in the shape of the reference's
+// test/unit/long_reduce.cpp (source produced on the device, reduced from inside the kernel by one
+// work-group per PE, checked against the closed form ((1 << npes) - 1) << 40 + idx * npes) and
+// of its reduce_*.cpp pattern tests (sources = reference source patterns, checked against the
+// reference check patterns restated in oracle/oracle.c, linked here as the CHECKER).
+// Launch: ISHMEM_PE=<pe> ISHMEM_NPES=<n> ISHMEM_DEVICE=0 ISHMEM_BOOTSTRAP_KEY=<k> ./device_wg
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "ishmem.h"
+#include "ishmemx_device.h"
+
+extern "C" {
+#include "oracle.h"
+}
+
+static int errors = 0;
+
+// long_reduce.cpp:78-79 / :120-127 — produce, then reduce, in one kernel.
+__global__ void long_reduce_kernel(const ishmemi_c_device_ctx_t *ctx, long *dest, long *source,
+                                   size_t n, int my_pe, int *rc)
+{
+    for (size_t i = threadIdx.x; i < n; i += blockDim.x) source[i] = (1L << (40 + my_pe)) + (long) i;
+    const int r = ishmemx_long_sum_reduce_work_group(ctx, dest, (const long *) source, n);
+    if (threadIdx.x == 0) *rc = r;
+}
+
+template <typename T, int OPC>
+__global__ void pattern_kernel(const ishmemi_c_device_ctx_t *ctx, int team, T *dest, const T *source,
+                               size_t n, int *rc)
+{
+    int r;
+    if constexpr (OPC == ISHMEMI_OP_SUM) r = ishmemx_sum_reduce_work_group(ctx, team, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_MAX) r = ishmemx_max_reduce_work_group(ctx, team, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_MIN) r = ishmemx_min_reduce_work_group(ctx, team, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_PROD) r = ishmemx_prod_reduce_work_group(ctx, team, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_AND) r = ishmemx_and_reduce_work_group(ctx, team, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_OR) r = ishmemx_or_reduce_work_group(ctx, team, dest, source, n);
+    else r = ishmemx_xor_reduce_work_group(ctx, team, dest, source, n);
+    if (threadIdx.x == 0) *rc = r;
+}
+
+template <typename T, int OPC, int ODT>
+static void pattern_case(const ishmemi_c_device_ctx_t *ctx, size_t n, int block, char *sb, char *db,
+                         int *rc)
+{
+    const int pe = ishmem_my_pe(), npes = ishmem_n_pes();
+    const int fam = OPC == OR_AND ? PAT_AND : OPC == OR_OR ? PAT_OR : OPC == OR_XOR ? PAT_XOR : PAT_ARITH;
+    std::vector<T> src(n), chk(n), got(n);
+    oracle_pattern_source(fam, ODT, pe, n, src.data());
+    oracle_pattern_check(fam, OPC, ODT, npes, n, chk.data());
+    (void) hipMemcpy(sb, src.data(), n * sizeof(T), hipMemcpyHostToDevice);
+    (void) hipMemset(db, 0, n * sizeof(T));
+    hipLaunchKernelGGL((pattern_kernel<T, OPC>), dim3(1), dim3(block), 0, 0, ctx, ISHMEM_TEAM_WORLD,
+                       (T *) db, (const T *) sb, n, rc);
+    (void) hipDeviceSynchronize();
+    int r = -1;
+    (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);
+    (void) hipMemcpy(got.data(), db, n * sizeof(T), hipMemcpyDeviceToHost);
+    if (r != 0 || memcmp(got.data(), chk.data(), n * sizeof(T)) != 0) {
+        if (++errors <= 16) printf("[%d] FAIL device pattern op %d dt %d n %zu rc %d\n", pe, OPC, ODT, n, r);
+    }
+}
+
+int main()
+{
+    ishmem_init();
+    const int pe = ishmem_my_pe(), npes = ishmem_n_pes();
+    if (pe < 0) {
+        printf("init failed: %s\n", ishmemi_c_last_error());
+        return 2;
+    }
+    const auto *ctx = (const ishmemi_c_device_ctx_t *) ishmemi_c_device_ctx();
+    const size_t maxn = 1 << 17;
+    char *sb = (char *) ishmem_malloc(maxn * 8);
+    char *db = (char *) ishmem_malloc(maxn * 8);
+    int *rc = (int *) ishmem_malloc(sizeof(int));
+
+    for (size_t n = 1; n <= maxn; n <<= 2) {
+        for (int block : {64, 256, 1024}) {
+            hipLaunchKernelGGL(long_reduce_kernel, dim3(1), dim3(block), 0, 0, ctx, (long *) db, (long *) sb,
+                               n, pe, rc);
+            (void) hipDeviceSynchronize();
+            std::vector<long> got(n);
+            int r = -1;
+            (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);
+            (void) hipMemcpy(got.data(), db, n * sizeof(long), hipMemcpyDeviceToHost);
+            const long mask = ((1L << npes) - 1) << 40;
+            size_t bad = 0;
+            for (size_t i = 0; i < n; ++i) bad += got[i] != mask + (long) i * npes;
+            if (r != 0 || bad) {
+                if (++errors <= 16) printf("[%d] FAIL long_reduce n %zu block %d rc %d bad %zu\n", pe, n, block, r, bad);
+            }
+        }
+    }
+    for (size_t n : {1, 7, 64, 1000, 4097}) {
+        pattern_case<float, OR_SUM, OD_FLOAT>(ctx, n, 256, sb, db, rc);
+        pattern_case<double, OR_PROD, OD_DOUBLE>(ctx, n, 256, sb, db, rc);
+        pattern_case<int32_t, OR_MIN, OD_INT32>(ctx, n, 128, sb, db, rc);
+        pattern_case<int8_t, OR_MAX, OD_INT8>(ctx, n, 256, sb, db, rc);
+        pattern_case<int16_t, OR_SUM, OD_INT16>(ctx, n, 64, sb, db, rc);
+        pattern_case<uint64_t, OR_XOR, OD_UINT64>(ctx, n, 512, sb, db, rc);
+        pattern_case<uint8_t, OR_AND, OD_UINT8>(ctx, n, 256, sb, db, rc);
+        pattern_case<uint32_t, OR_OR, OD_UINT32>(ctx, n, 256, sb, db, rc);
+    }
+    ishmem_free(rc);
+    ishmem_free(db);
+    ishmem_free(sb);
+    ishmem_barrier_all();
+    if (ishmemi_c_error_count()) ++errors;
+    printf("[%d] %s errors %d\n", pe, errors ? "FAIL" : "PASS", errors);
+    ishmem_finalize();
+    return errors ? 1 : 0;
+}

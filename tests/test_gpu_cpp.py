@@ -10,35 +10,31 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 EXE = ROOT / "build" / "reduce_patterns"
+DEV_EXE = ROOT / "build" / "device_wg"
+HEADERS = [ROOT / "include/ishmem.h", ROOT / "include/ishmemx.h", ROOT / "include/ishmem_capi.h",
+           ROOT / "include/ishmemx_device.h", ROOT / "oracle/oracle.c", ROOT / "oracle/oracle.h"]
 
 
-def build_exe() -> Path:
-    srcs = [ROOT / "tests/cpp/reduce_patterns.cpp", ROOT / "oracle/oracle.c", ROOT / "oracle/oracle.h",
-            ROOT / "include/ishmem.h", ROOT / "include/ishmemx.h", ROOT / "include/ishmem_capi.h"]
-    if EXE.exists() and all(s.stat().st_mtime <= EXE.stat().st_mtime for s in srcs):
-        return EXE
-    EXE.parent.mkdir(parents=True, exist_ok=True)
-    obj = EXE.parent / "oracle_for_cpp_test.o"
+def build_exe(src: Path = ROOT / "tests/cpp/reduce_patterns.cpp", exe: Path = EXE) -> Path:
+    """hipcc the test program against include/ and libishmem_amd.so; link the oracle (checker)."""
+    deps = [src, *HEADERS, ROOT / "ishmem_amd/libishmem_amd.so"]
+    if exe.exists() and all(s.stat().st_mtime <= exe.stat().st_mtime for s in deps if s.exists()):
+        return exe
+    exe.parent.mkdir(parents=True, exist_ok=True)
+    obj = exe.parent / "oracle_for_cpp_test.o"
     subprocess.run(["gcc", "-O2", "-std=gnu11", "-fPIC", "-c", str(ROOT / "oracle/oracle.c"), "-o", str(obj)],
                    check=True)
-    tobj = EXE.parent / "reduce_patterns.o"
+    tobj = exe.with_suffix(".o")
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-O2", "-std=c++20", "-Wno-unused-value",
-                    f"-I{ROOT / 'include'}", f"-I{ROOT / 'oracle'}", "-c",
-                    str(ROOT / "tests/cpp/reduce_patterns.cpp"), "-o", str(tobj)], check=True)
-    subprocess.run(["hipcc", "--offload-arch=gfx950", str(tobj), str(obj), f"-L{ROOT / 'ishmem_amd'}",
-                    "-lishmem_amd", "-lm", "-lpthread", f"-Wl,-rpath,{ROOT / 'ishmem_amd'}", "-o", str(EXE)],
+                    f"-I{ROOT / 'include'}", f"-I{ROOT / 'oracle'}", "-c", str(src), "-o", str(tobj)],
                    check=True)
-    return EXE
+    subprocess.run(["hipcc", "--offload-arch=gfx950", str(tobj), str(obj), f"-L{ROOT / 'ishmem_amd'}",
+                    "-lishmem_amd", "-lm", "-lpthread", f"-Wl,-rpath,{ROOT / 'ishmem_amd'}", "-o", str(exe)],
+                   check=True)
+    return exe
 
 
-def test_cpp_test_program_builds():
-    assert build_exe().exists()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("npes", [2])
-def test_cpp_reference_style_reduce_tests(npes):
-    exe = build_exe()
+def run_exe(exe: Path, npes: int, timeout: float = 600) -> None:
     key = f"cpp{uuid.uuid4().hex[:10]}"
     procs = []
     for pe in range(npes):
@@ -50,7 +46,7 @@ def test_cpp_reference_style_reduce_tests(npes):
     outs = []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=600)
+            out, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
             p.kill()
             out, _ = p.communicate()
@@ -58,3 +54,24 @@ def test_cpp_reference_style_reduce_tests(npes):
     for rc, out in outs:
         assert rc == 0, out[-3000:]
         assert "PASS errors 0" in out
+
+
+def test_cpp_test_program_builds():
+    assert build_exe().exists()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npes", [2])
+def test_cpp_reference_style_reduce_tests(npes):
+    run_exe(build_exe(), npes)
+
+
+def test_device_api_program_builds():
+    assert build_exe(ROOT / "tests/cpp/device_wg.hip", DEV_EXE).exists()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npes", [2, 3])
+def test_device_initiated_work_group_reduce(npes):
+    """ishmemx_*_reduce_work_group called from a user kernel (include/ishmemx_device.h)."""
+    run_exe(build_exe(ROOT / "tests/cpp/device_wg.hip", DEV_EXE), npes)
