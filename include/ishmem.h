@@ -10,8 +10,8 @@
  * fixed-width integer types only; schar bitwise is declared by the reference but never defined,
  * reduce.cpp:97-110, so it is not provided here either).
  *
- * Host-callable only: the reference's device-callable overloads (SYCL_EXTERNAL) are replaced by
- * kernels the library launches itself; see ishmemx.h for the stream-ordered variant.
+ * Host-callable.  The stream-ordered variant is in ishmemx.h; the device-callable work-group
+ * reductions (the reference's SYCL_EXTERNAL *_work_group overloads) are in ishmemx_device.h.
  */
 #ifndef ISHMEM_AMD_ISHMEM_H
 #define ISHMEM_AMD_ISHMEM_H
@@ -53,6 +53,13 @@ inline int ishmem_team_split_strided(ishmem_team_t parent_team, int start, int s
                                      ishmem_team_t *new_team)
 {
     return ishmemi_c_team_split_strided(parent_team, start, stride, size, new_team);
+}
+inline int ishmem_team_split_2d(ishmem_team_t parent_team, int xrange, const void * /*xaxis_config*/,
+                                long /*xaxis_mask*/, ishmem_team_t *xaxis_team,
+                                const void * /*yaxis_config*/, long /*yaxis_mask*/,
+                                ishmem_team_t *yaxis_team)
+{
+    return ishmemi_c_team_split_2d(parent_team, xrange, xaxis_team, yaxis_team);
 }
 inline void ishmem_team_destroy(ishmem_team_t team) { ishmemi_c_team_destroy(team); }
 

@@ -93,6 +93,7 @@ int ishmemi_c_team_my_pe(int team);
 int ishmemi_c_team_n_pes(int team);
 int ishmemi_c_team_translate_pe(int src_team, int src_pe, int dest_team);
 int ishmemi_c_team_split_strided(int parent_team, int start, int stride, int size, int *new_team);
+int ishmemi_c_team_split_2d(int parent_team, int xrange, int *xaxis_team, int *yaxis_team);
 void ishmemi_c_team_destroy(int team);
 
 /* ---- synchronisation — ishmem_barrier_all / sync_all / team_sync (src/ishmem.h:1555-1559,

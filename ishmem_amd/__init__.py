@@ -141,6 +141,13 @@ def ishmem_team_split_strided(parent: int, start: int, stride: int, size: int) -
     return r, t.value
 
 
+def ishmem_team_split_2d(parent: int, xrange: int) -> tuple[int, int, int]:
+    """Returns (status, xaxis_team, yaxis_team) (src/teams.cpp:453-518)."""
+    x, y = ctypes.c_int(-1), ctypes.c_int(-1)
+    r = _L.ishmemi_c_team_split_2d(parent, xrange, ctypes.byref(x), ctypes.byref(y))
+    return r, x.value, y.value
+
+
 def ishmem_team_destroy(team: int) -> None:
     _L.ishmemi_c_team_destroy(team)
 

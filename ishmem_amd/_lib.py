@@ -30,6 +30,7 @@ PROTOTYPES = [
     ("ishmemi_c_team_n_pes", _i, [_i]),
     ("ishmemi_c_team_translate_pe", _i, [_i, _i, _i]),
     ("ishmemi_c_team_split_strided", _i, [_i, _i, _i, _i, ctypes.POINTER(_i)]),
+    ("ishmemi_c_team_split_2d", _i, [_i, _i, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     ("ishmemi_c_team_destroy", None, [_i]),
     ("ishmemi_c_barrier_all", _i, []),
     ("ishmemi_c_sync_all", _i, []),

@@ -109,6 +109,7 @@ struct State {
     ishmemi_c_device_ctx_t *dctx = nullptr;  // device copy of the device-API context
     uint32_t *dev_epochs = nullptr;
 
+    char *team_scratch = nullptr;  // small symmetric buffer for team-management collectives
     char *staging = nullptr;  // symmetric staging region for non-heap / host buffers
     size_t staging_bytes = 0;
     hipStream_t copy_in = nullptr, copy_out = nullptr;  // staging pipeline streams
@@ -551,13 +552,17 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             if (all[j].heap_size != s.heap_size)
                 return fail("init: ISHMEM_SYMMETRIC_SIZE differs between PEs");
             if (all[j].device != s.device) {
+                // The kernels load peers' memory directly over xGMI: without peer access those
+                // loads would fault the GPU, so refuse to initialise instead.
                 int can = 0;
-                if (hipDeviceCanAccessPeer(&can, s.device, all[j].device) == hipSuccess && can) {
-                    hipError_t e = hipDeviceEnablePeerAccess(all[j].device, 0);
-                    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-                        return hipfail("hipDeviceEnablePeerAccess", e);
-                    (void) hipGetLastError();
-                }
+                if (hipDeviceCanAccessPeer(&can, s.device, all[j].device) != hipSuccess || !can)
+                    return fail("init: no peer access from device " + std::to_string(s.device) +
+                                " to device " + std::to_string(all[j].device) + " (PE " +
+                                std::to_string(j) + ")");
+                hipError_t e = hipDeviceEnablePeerAccess(all[j].device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                    return hipfail("hipDeviceEnablePeerAccess", e);
+                (void) hipGetLastError();
             }
             HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_heap[j], all[j].heap_handle,
                                         hipIpcMemLazyEnablePeerAccess));
@@ -581,6 +586,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.staging_bytes = parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20);
     s.staging = (char *) heap_alloc(s, s.staging_bytes, kHeapAlign);
     if (!s.staging) return 1;
+    s.team_scratch = (char *) heap_alloc(s, kHeapAlign, kHeapAlign);
+    if (!s.team_scratch) return 1;
     HIP_TRY(hipMalloc((void **) &s.dctx, sizeof(ishmemi_c_device_ctx_t)));
     HIP_TRY(hipMalloc((void **) &s.dev_epochs, kMaxTeams * sizeof(uint32_t)));
     HIP_TRY(hipMemset(s.dev_epochs, 0, kMaxTeams * sizeof(uint32_t)));
@@ -776,9 +783,11 @@ int ishmemi_c_team_translate_pe(int src_team, int src_pe, int dest_team)
 
 int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, int *new_team)
 {
+    // Collective over the parent team (src/teams.cpp:294-452).
     State &s = S();
     if (new_team) *new_team = ISHMEMI_C_TEAM_INVALID;
-    int slot = -1;
+    uint64_t free_mask = 0;
+    Team t;
     {
         std::lock_guard<std::mutex> lk(s.mu);
         if (!s.initialized) return fail("team_split_strided: not initialized");
@@ -786,24 +795,38 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
             return fail("team_split_strided: invalid parent team");
         const Team &pt = s.teams[parent];
         if (pt.my_idx < 0) return fail("team_split_strided: caller not in parent team");
-        if (size < 1 || start < 0 || start >= pt.size || (size > 1 && stride < 1) ||
-            start + (size - 1) * std::max(stride, 0) >= pt.size)
-            return fail("team_split_strided: invalid triplet");
-        for (int i = ISHMEMI_C_TEAM_NODE + 1; i < kMaxTeams; ++i)
-            if (!s.teams[i].valid) {
-                slot = i;
-                break;
-            }
-        if (slot < 0) return fail("team_split_strided: no free team slot");
-        Team t;
+        stride = (stride == 0 || size == 1) ? 1 : stride;  // teams.cpp:304
+        const int gstart = pt.start + start * pt.stride;
+        const int gstride = pt.stride * stride;
+        const int gend = gstart + gstride * (size - 1);
+        if (start < 0 || start >= pt.size || size <= 0 || size > pt.size || gstart < 0 ||
+            gstart >= s.npes || gend < 0 || gend >= s.npes)  // teams.cpp:309-325
+            return fail("team_split_strided: invalid <start, stride, size>");
         t.valid = true;
-        t.start = pt.start + start * pt.stride;
-        t.stride = (size > 1 ? stride : 1) * pt.stride;
+        t.start = gstart;
+        t.stride = gstride;
         t.size = size;
-        const int d = s.pe - t.start;
-        t.my_idx = (d >= 0 && d % t.stride == 0 && d / t.stride < size) ? d / t.stride : -1;
-        t.epoch = 0;
-        s.teams[slot] = t;
+        const int d = s.pe - gstart;
+        t.my_idx = (d % gstride == 0 && d / gstride >= 0 && d / gstride < size) ? d / gstride : -1;
+        for (int i = ISHMEMI_C_TEAM_NODE + 1; i < kMaxTeams; ++i)
+            if (!s.teams[i].valid) free_mask |= 1ull << i;
+    }
+    // Agree on a slot free on every parent member: AND-reduce the free masks over the parent
+    // team with the library's own reduction (the reference's bit reduction, teams.cpp:327-345).
+    if (hipMemcpy(s.team_scratch, &free_mask, 8, hipMemcpyHostToDevice) != hipSuccess)
+        return fail("team_split_strided: mask copy failed");
+    if (ishmemi_c_reduce(parent, ISHMEMI_OP_AND, ISHMEMI_DT_UINT64, s.team_scratch, s.team_scratch, 1))
+        return 1;
+    if (hipMemcpy(&free_mask, s.team_scratch, 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail("team_split_strided: mask copy failed");
+    if (!free_mask) return fail("team_split_strided: no team slot free on every parent member");
+    const int slot = __builtin_ctzll(free_mask);
+    {
+        std::lock_guard<std::mutex> lk(s.mu);
+        // Only members hold the slot.  A later team that reuses it on a non-member is disjoint
+        // from this team (every member of this one has the slot reserved, so the AND-reduced
+        // mask of any parent containing one of them excludes it): flag blocks never collide.
+        if (t.my_idx >= 0) s.teams[slot] = t;
         // Fresh flag block: zero it locally, then the parent sync below orders the zeroing
         // before any member's first barrier on the new team.
         if (hipMemset(team_flags(s.flags, slot), 0, kTeamFlagBytes) != hipSuccess ||
@@ -815,7 +838,38 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
         if (hipDeviceSynchronize() != hipSuccess) return fail("team_split_strided: sync failed");
     }
     if (ishmemi_c_team_sync(parent)) return 1;
-    if (new_team && s.teams[slot].my_idx >= 0) *new_team = slot;
+    if (new_team && t.my_idx >= 0) *new_team = slot;
+    return 0;
+}
+
+int ishmemi_c_team_split_2d(int parent, int xrange, int *xaxis_team, int *yaxis_team)
+{
+    // src/teams.cpp:453-518: x-axis teams are contiguous groups of xrange parent PEs, y-axis
+    // teams take every xrange-th parent PE; both are split_strided calls over the parent.
+    State &s = S();
+    if (xaxis_team) *xaxis_team = ISHMEMI_C_TEAM_INVALID;
+    if (yaxis_team) *yaxis_team = ISHMEMI_C_TEAM_INVALID;
+    if (!s.initialized) return fail("team_split_2d: not initialized");
+    if (parent < 0 || parent >= kMaxTeams || !s.teams[parent].valid)
+        return fail("team_split_2d: invalid parent team");
+    if (xrange < 1) return fail("team_split_2d: xrange must be >= 1");
+    const int psize = s.teams[parent].size;
+    if (xrange > psize) xrange = psize;
+    const int nx = (psize + xrange - 1) / xrange, ny = xrange;
+    int start = 0;
+    for (int i = 0; i < nx; ++i, start += xrange) {
+        const int xsize = (i == nx - 1 && psize % xrange) ? psize % xrange : xrange;
+        int t = ISHMEMI_C_TEAM_INVALID;
+        if (ishmemi_c_team_split_strided(parent, start, 1, xsize, &t)) return 1;
+        if (t != ISHMEMI_C_TEAM_INVALID && xaxis_team) *xaxis_team = t;
+    }
+    for (int i = 0; i < ny; ++i) {
+        const int rem = psize % xrange, yr = psize / xrange;
+        const int ysize = (rem && i < rem) ? yr + 1 : yr;
+        int t = ISHMEMI_C_TEAM_INVALID;
+        if (ishmemi_c_team_split_strided(parent, i, xrange, ysize, &t)) return 1;
+        if (t != ISHMEMI_C_TEAM_INVALID && yaxis_team) *yaxis_team = t;
+    }
     return 0;
 }
 

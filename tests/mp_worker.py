@@ -195,9 +195,40 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                     fails.append(f"pe{pe} team reduce rc={r} {ish.last_error()}")
                 else:
                     check("team", OPS["sum"], DT["int64"], [ins[j] for j in members], hip.download(d, n, np.int64))
-                ish.ishmem_team_destroy(team)
             elif pe % 2 == 0:
                 fails.append(f"pe{pe} should be in the even team")
+            # Nested split of the even team (members 0, 2, ...): its second member alone.  All
+            # PEs must still agree on team slots afterwards (free-mask AND-reduction).
+            if team != ish.ISHMEM_TEAM_INVALID and size >= 2:
+                r, solo = ish.ishmem_team_split_strided(team, 1, 1, 1)
+                if r or (solo != ish.ISHMEM_TEAM_INVALID) != (pe == 2):
+                    fails.append(f"pe{pe} nested split rc={r} team={solo}")
+                if solo != ish.ISHMEM_TEAM_INVALID:
+                    ish.ishmem_team_destroy(solo)
+            if team != ish.ISHMEM_TEAM_INVALID:
+                ish.ishmem_team_destroy(team)
+            # 2-D split of WORLD (src/teams.cpp:453-518), xrange 2: x-teams {0,1},{2,3},...;
+            # y-teams {0,2,..},{1,3,..}; reduce over both axes.
+            r, xt, yt = ish.ishmem_team_split_2d(ish.ISHMEM_TEAM_WORLD, 2)
+            if r or xt == ish.ISHMEM_TEAM_INVALID or yt == ish.ISHMEM_TEAM_INVALID:
+                fails.append(f"pe{pe} split_2d rc={r} x={xt} y={yt} {ish.last_error()}")
+            else:
+                xm = [j for j in range(npes) if j // 2 == pe // 2]
+                ym = [j for j in range(npes) if j % 2 == pe % 2]
+                if ish.ishmem_team_n_pes(xt) != len(xm) or ish.ishmem_team_n_pes(yt) != len(ym):
+                    fails.append(f"pe{pe} split_2d sizes")
+                if ish.ishmem_team_translate_pe(xt, 0, ish.ISHMEM_TEAM_WORLD) != xm[0]:
+                    fails.append(f"pe{pe} translate_pe")
+                for tm, members in ((xt, xm), (yt, ym)):
+                    allin = {j: oracle.fill_random(DT["int64"], 90 + j, n) for j in range(npes)}
+                    hip.upload(s, allin[pe])
+                    if ish.ishmem_int64_sum_reduce(tm, d, s, n):
+                        fails.append(f"pe{pe} 2d reduce failed {ish.last_error()}")
+                    else:
+                        check("2d", OPS["sum"], DT["int64"], [allin[j] for j in members],
+                              hip.download(d, n, np.int64))
+                ish.ishmem_team_destroy(xt)
+                ish.ishmem_team_destroy(yt)
             ish.ishmem_free(d)
             ish.ishmem_free(s)
 
