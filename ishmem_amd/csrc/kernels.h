@@ -43,6 +43,25 @@ struct ReduceArgs {
     int p, me;
 };
 
+// Small-message ("LL") path: 8-byte granules {4 data bytes | 32-bit epoch} pushed into every
+// peer's fine-grained receive ring; [parity 2][sender kMaxPes][kLLGranules] u64 per team.
+constexpr size_t kLLMaxBytes = 16384;                 // payload bytes per PE handled by LL
+constexpr size_t kLLGranules = kLLMaxBytes / 4;       // 4 payload bytes per granule
+constexpr size_t kLLTeamBytes = (size_t) 2 * kMaxPes * kLLGranules * 8;  // 1 MiB
+struct LLArgs {
+    const char *src;
+    char *dst;
+    uint64_t *my_ring;              // this team's ring base on this PE (parity 0, sender 0)
+    uint64_t *peer_ring[kMaxPes];   // the same ring base on every member, mapped here
+    uint32_t *err;
+    int *ret;
+    uint64_t nbytes;
+    uint64_t timeout_ticks;
+    uint32_t epoch;
+    int p, me;
+};
+hipError_t launch_ll(int op, int dt, const LLArgs &a, hipStream_t s);
+
 // Arguments of the local k-input fan-in combine: dst = op(src0, src1, ..., src_{k-1}).
 constexpr int kMaxFanin = 16;
 struct FaninArgs {

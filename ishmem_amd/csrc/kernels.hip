@@ -7,7 +7,8 @@ namespace ishmemi {
 #define ISHMEMI_DECL_OP(N)                                                                         \
     hipError_t launch_allreduce_op##N(int dt, bool vec, const ReduceArgs &a, int grid,             \
                                       hipStream_t s);                                              \
-    hipError_t launch_fanin_op##N(int dt, bool vec, const FaninArgs &a, int grid, hipStream_t s);
+    hipError_t launch_fanin_op##N(int dt, bool vec, const FaninArgs &a, int grid, hipStream_t s); \
+    hipError_t launch_ll_op##N(int dt, const LLArgs &a, hipStream_t s);
 ISHMEMI_DECL_OP(0)
 ISHMEMI_DECL_OP(1)
 ISHMEMI_DECL_OP(2)
@@ -42,6 +43,21 @@ hipError_t launch_fanin(int op, int dt, bool vec, const FaninArgs &a, int grid, 
         case 4: return launch_fanin_op4(dt, vec, a, grid, s);
         case 5: return launch_fanin_op5(dt, vec, a, grid, s);
         case 6: return launch_fanin_op6(dt, vec, a, grid, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_ll(int op, int dt, const LLArgs &a, hipStream_t s)
+{
+    if (!op_dtype_valid(op, dt)) return hipErrorInvalidValue;
+    switch (op) {
+        case 0: return launch_ll_op0(dt, a, s);
+        case 1: return launch_ll_op1(dt, a, s);
+        case 2: return launch_ll_op2(dt, a, s);
+        case 3: return launch_ll_op3(dt, a, s);
+        case 4: return launch_ll_op4(dt, a, s);
+        case 5: return launch_ll_op5(dt, a, s);
+        case 6: return launch_ll_op6(dt, a, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -455,6 +455,89 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Small-message path: one data hop, no barriers.  Thread t owns 8 payload bytes (item t): it
+// pushes them as two {data, epoch} granules into slot `me` of every peer's ring (system-scope
+// 8-B atomic stores into fine-grained memory: a granule is its own flag, MI355X_MICROARCH.md
+// R2), then polls its own ring until all p-1 peers' granules for item t carry this epoch and
+// folds the p items in canonical team order.  Sources are reusable at once (they were copied);
+// ring parity = epoch & 1, and a peer can be at most one collective ahead (it cannot finish
+// collective e+1 without our e+1 push), so two parities never collide.
+// ---------------------------------------------------------------------------------------------
+template <typename T, int OP>
+__device__ __forceinline__ uint64_t fold8(uint64_t acc, uint64_t x)
+{
+    constexpr int K = 8 / sizeof(T);
+    struct alignas(8) W {
+        T e[K];
+    };
+    W a = __builtin_bit_cast(W, acc), b = __builtin_bit_cast(W, x);
+#pragma unroll
+    for (int i = 0; i < K; ++i) a.e[i] = op1<T, OP>(a.e[i], b.e[i]);
+    return __builtin_bit_cast(uint64_t, a);
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
+{
+    const uint64_t item = (uint64_t) blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t nitems = (a.nbytes + 7) / 8;
+    const int p = a.p, me = a.me;
+    const uint64_t par = a.epoch & 1u;
+    const uint64_t tag = (uint64_t) a.epoch << 32;
+    bool ok = true;
+    if (item < nitems) {
+        const uint64_t off = item * 8;
+        const uint64_t valid = a.nbytes - off < 8 ? a.nbytes - off : 8;
+        uint64_t mine = 0;
+        if (valid == 8) mine = *(const uint64_t *) (a.src + off);
+        else memcpy(&mine, a.src + off, valid);
+        const uint64_t g0 = tag | (uint32_t) mine, g1 = tag | (uint32_t) (mine >> 32);
+        for (int j = 0; j < p; ++j) {
+            if (j == me) continue;
+            uint64_t *slot = a.peer_ring[j] + (par * kMaxPes + me) * kLLGranules + 2 * item;
+            __hip_atomic_store(slot, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(slot + 1, g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        uint64_t acc = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (int j = 0; j < p && ok; ++j) {
+            uint64_t x = mine;
+            if (j != me) {
+                const uint64_t *slot = a.my_ring + (par * kMaxPes + j) * kLLGranules + 2 * item;
+                uint64_t h0, h1;
+                for (;;) {
+                    h0 = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    h1 = __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if ((h0 >> 32) == a.epoch && (h1 >> 32) == a.epoch) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+                        ok = false;
+                        __hip_atomic_fetch_or(a.err, 1u << 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                x = (h0 & 0xffffffffull) | (h1 << 32);
+            }
+            acc = (j == 0) ? x : fold8<T, OP>(acc, x);
+        }
+        if (ok) {
+            if (valid == 8) *(uint64_t *) (a.dst + off) = acc;
+            else memcpy(a.dst + off, &acc, valid);
+        }
+    }
+    if (a.ret && blockIdx.x == 0 && threadIdx.x == 0) *a.ret = ok ? 0 : 1;
+}
+
+template <typename T, int OP>
+hipError_t ll_t(const LLArgs &a, hipStream_t s)
+{
+    const uint64_t nitems = (a.nbytes + 7) / 8;
+    const int grid = (int) ((nitems + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL((ll_kernel<T, OP>), dim3(grid > 0 ? grid : 1), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
 // Standalone team barrier (ishmem_team_sync / barrier_all analogue): one workgroup.
 __global__ __launch_bounds__(kBlock) void team_sync_kernel(ReduceArgs a)
 {

@@ -24,4 +24,10 @@ hipError_t ISHMEMI_CAT(launch_fanin_op, ISHMEMI_KOP)(int dt, bool vec, const Fan
     return dispatch_dt<ISHMEMI_KOP, FaninArgs>(dt, l);
 }
 
+hipError_t ISHMEMI_CAT(launch_ll_op, ISHMEMI_KOP)(int dt, const LLArgs &a, hipStream_t s)
+{
+    auto l = [&]<typename T, int OP>() { return ll_t<T, OP>(a, s); };
+    return dispatch_dt<ISHMEMI_KOP, LLArgs>(dt, l);
+}
+
 }  // namespace ishmemi

@@ -30,6 +30,9 @@ static_assert(kMaxPes == ISHMEMI_C_MAX_PES, "device ctx layout");
 // fine-grained, IPC-shared allocation.
 constexpr size_t kDevFlagWordsPerTeam = (size_t) ISHMEMI_C_DEV_PHASES * kMaxPes;
 constexpr size_t kDevFlagBytes = (size_t) kMaxTeams * kDevFlagWordsPerTeam * 4;
+// Small-message rings (kernels.h: kLLTeamBytes per team) follow, 256-B aligned.
+constexpr size_t kLLOffset = ((size_t) kMaxTeams * kTeamFlagBytes + kDevFlagBytes + 255) & ~(size_t) 255;
+constexpr size_t kFlagAllocBytes = kLLOffset + (size_t) kMaxTeams * kLLTeamBytes;
 constexpr size_t kHeapAlign = 256;
 
 thread_local std::string g_last_error;
@@ -117,6 +120,7 @@ struct State {
 
     Team teams[kMaxTeams];
     int max_blocks = kMaxBlocks;
+    long long ll_max_bytes = (long long) kLLMaxBytes;
     long long timeout_ms = 60000;
     int debug = 0;
     int error_count = 0;
@@ -140,6 +144,12 @@ char *translate(const State &s, const void *p, int pe)
     if (pe == s.pe) return (char *) p;
     if (pe < 0 || pe >= s.npes || !s.peer_heap[pe]) return nullptr;
     return s.peer_heap[pe] + ((const char *) p - s.heap);
+}
+
+uint64_t *ll_ring(uint32_t *flags_base, int team)
+{
+    return flags_base ? (uint64_t *) ((char *) flags_base + kLLOffset + (size_t) team * kLLTeamBytes)
+                      : nullptr;
 }
 
 uint32_t *team_flags(uint32_t *base, int team)
@@ -307,6 +317,40 @@ int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)
     return 0;
 }
 
+// Small payloads (<= ll_max_bytes, 8-B aligned, device memory anywhere): one-hop push of
+// {data, epoch} granules into the peers' rings, no barriers (ll_kernel).
+bool ll_eligible(const State &s, const Team &t, const void *dst, const void *src, size_t bytes)
+{
+    return t.size > 1 && bytes > 0 && (long long) bytes <= s.ll_max_bytes &&
+           bytes <= kLLMaxBytes && (((uintptr_t) dst | (uintptr_t) src) & 7) == 0;
+}
+
+int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, size_t bytes, int *ret,
+              hipStream_t st)
+{
+    Team &t = s.teams[team];
+    LLArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = (const char *) src;
+    a.dst = (char *) dst;
+    a.my_ring = ll_ring(s.flags, team);
+    for (int j = 0; j < t.size; ++j) {
+        const int gpe = t.start + j * t.stride;
+        a.peer_ring[j] = ll_ring(s.peer_flags[gpe], team);
+        if (!a.peer_ring[j]) return fail("reduce: PE " + std::to_string(gpe) + " ring not mapped");
+    }
+    a.err = s.err_dev + team;
+    a.ret = ret;
+    a.nbytes = bytes;
+    a.timeout_ticks = (uint64_t) s.timeout_ms * 100000ull;
+    if (++t.epoch == 0) t.epoch = 1;
+    a.epoch = t.epoch;
+    a.p = t.size;
+    a.me = t.my_idx;
+    HIP_TRY(launch_ll(op, dt, a, st));
+    return 0;
+}
+
 // Device-resident collective on symmetric-heap buffers: one allreduce_kernel launch.
 int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, size_t n, int *ret,
                 hipStream_t st)
@@ -369,7 +413,12 @@ int reduce_staged(State &s, int team, int op, int dt, void *dst, const void *src
         HIP_TRY(hipEventRecord(s.ev_in[sl], s.copy_in));
         HIP_TRY(hipStreamWaitEvent(st, s.ev_in[sl], 0));
         // One PE: the in-place reduce of the staged chunk is the identity (reduce_impl.h:288-289).
-        if (s.teams[team].size > 1 && reduce_heap(s, team, op, dt, buf, buf, m, ret, st)) return 1;
+        if (s.teams[team].size > 1) {
+            const bool ll = ll_eligible(s, s.teams[team], buf, buf, m * es);
+            if (ll ? reduce_ll(s, team, op, dt, buf, buf, m * es, ret, st)
+                   : reduce_heap(s, team, op, dt, buf, buf, m, ret, st))
+                return 1;
+        }
         HIP_TRY(hipEventRecord(s.ev_red[sl], st));
         HIP_TRY(hipStreamWaitEvent(s.copy_out, s.ev_red[sl], 0));
         HIP_TRY(hipMemcpyAsync((char *) dst + off * es, buf, m * es, hipMemcpyDefault, s.copy_out));
@@ -424,6 +473,9 @@ int reduce_impl(int team, int op, int dt, void *dst, const void *src, size_t n, 
     } else if (n == 0) {
         // The reference still synchronises the team (reduce_impl.h:244, :254).
         if (team_sync_locked(s, team, st, ret)) return 1;
+    } else if (ll_eligible(s, t, dst, src, bytes) && classify(s, dst) != Kind::Host &&
+               classify(s, src) != Kind::Host) {
+        if (reduce_ll(s, team, op, dt, dst, src, bytes, ret, st)) return 1;
     } else if (in_heap(s, dst) && in_heap(s, src)) {
         if (reduce_heap(s, team, op, dt, dst, src, n, ret, st)) return 1;
     } else {
@@ -480,6 +532,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.npes = npes;
     s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, env_ll("ISHMEM_MAX_BLOCKS", kMaxBlocks)));
     s.timeout_ms = std::max<long long>(1, env_ll("ISHMEM_TIMEOUT_MS", 60000));
+    s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
+                                         std::max<long long>(0, env_ll("ISHMEM_LL_MAX_BYTES", (long long) kLLMaxBytes)));
     s.debug = (int) env_ll("ISHMEM_DEBUG", 0);
 
     int ndev = 0;
@@ -497,7 +551,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.free_list[0] = s.heap_size;
 
     // Barrier flags: fine-grained (uncached) device memory, written by peers over xGMI.
-    const size_t flag_bytes = (size_t) kMaxTeams * kTeamFlagBytes + kDevFlagBytes;
+    const size_t flag_bytes = kFlagAllocBytes;
     if (hipExtMallocWithFlags((void **) &s.flags, flag_bytes, hipDeviceMallocUncached) == hipSuccess) {
         s.flags_fine_grained = true;
     } else {
@@ -832,7 +886,8 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
         if (hipMemset(team_flags(s.flags, slot), 0, kTeamFlagBytes) != hipSuccess ||
             hipMemset(dev_flags(s.flags) + (size_t) slot * kDevFlagWordsPerTeam, 0,
                       kDevFlagWordsPerTeam * 4) != hipSuccess ||
-            hipMemset(s.dev_epochs + slot, 0, sizeof(uint32_t)) != hipSuccess)
+            hipMemset(s.dev_epochs + slot, 0, sizeof(uint32_t)) != hipSuccess ||
+            hipMemset(ll_ring(s.flags, slot), 0, kLLTeamBytes) != hipSuccess)
             return fail("team_split_strided: flag reset failed");
         if (sync_device_ctx(s)) return 1;
         if (hipDeviceSynchronize() != hipSuccess) return fail("team_split_strided: sync failed");
@@ -951,6 +1006,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     const std::string n = name ? name : "";
     if (n == "max_blocks") s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, value));
     else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
+    else if (n == "ll_max_bytes") s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes, std::max<long long>(0, value));
     else if (n == "debug") s.debug = (int) value;
     else return fail("set_param: unknown parameter " + n);
     return 0;
@@ -962,6 +1018,7 @@ long long ishmemi_c_get_param(const char *name)
     const std::string n = name ? name : "";
     if (n == "max_blocks") return s.max_blocks;
     if (n == "timeout_ms") return s.timeout_ms;
+    if (n == "ll_max_bytes") return s.ll_max_bytes;
     if (n == "debug") return s.debug;
     if (n == "flags_fine_grained") return s.flags_fine_grained ? 1 : 0;
     if (n == "staging_bytes") return (long long) s.staging_bytes;
