@@ -175,4 +175,88 @@ ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_TYPED, min, ISHMEMI_OP_MIN)
 ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_TYPED, sum, ISHMEMI_OP_SUM)
 ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_TYPED, prod, ISHMEMI_OP_PROD)
 
+/* ---- fcollect / collect / scan (src/ishmem.h:894-921 and the scan section) ---- */
+inline int ishmem_fcollectmem(void *dest, const void *source, size_t nbytes)
+{
+    return ishmemi_c_fcollect(ISHMEM_TEAM_WORLD, dest, source, nbytes);
+}
+inline int ishmem_fcollectmem(ishmem_team_t team, void *dest, const void *source, size_t nbytes)
+{
+    return ishmemi_c_fcollect(team, dest, source, nbytes);
+}
+inline int ishmem_collectmem(void *dest, const void *source, size_t nbytes)
+{
+    return ishmemi_c_collect(ISHMEM_TEAM_WORLD, dest, source, nbytes);
+}
+inline int ishmem_collectmem(ishmem_team_t team, void *dest, const void *source, size_t nbytes)
+{
+    return ishmemi_c_collect(team, dest, source, nbytes);
+}
+template <typename T>
+inline int ishmem_fcollect(ishmem_team_t team, T *dest, const T *source, size_t nelems)
+{
+    return ishmemi_c_fcollect(team, (void *) dest, (const void *) source, nelems * sizeof(T));
+}
+template <typename T>
+inline int ishmem_fcollect(T *dest, const T *source, size_t nelems)
+{
+    return ishmem_fcollect(ISHMEM_TEAM_WORLD, dest, source, nelems);
+}
+template <typename T>
+inline int ishmem_collect(ishmem_team_t team, T *dest, const T *source, size_t nelems)
+{
+    return ishmemi_c_collect(team, (void *) dest, (const void *) source, nelems * sizeof(T));
+}
+template <typename T>
+inline int ishmem_collect(T *dest, const T *source, size_t nelems)
+{
+    return ishmem_collect(ISHMEM_TEAM_WORLD, dest, source, nelems);
+}
+template <typename T>
+inline int ishmem_sum_inscan(ishmem_team_t team, T *dest, const T *source, size_t nelems)
+{
+    return ishmemi_c_scan(team, ishmemi_cxx::dtype_of<T>(), 1, (void *) dest, (const void *) source, nelems);
+}
+template <typename T>
+inline int ishmem_sum_inscan(T *dest, const T *source, size_t nelems)
+{
+    return ishmem_sum_inscan(ISHMEM_TEAM_WORLD, dest, source, nelems);
+}
+template <typename T>
+inline int ishmem_sum_exscan(ishmem_team_t team, T *dest, const T *source, size_t nelems)
+{
+    return ishmemi_c_scan(team, ishmemi_cxx::dtype_of<T>(), 0, (void *) dest, (const void *) source, nelems);
+}
+template <typename T>
+inline int ishmem_sum_exscan(T *dest, const T *source, size_t nelems)
+{
+    return ishmem_sum_exscan(ISHMEM_TEAM_WORLD, dest, source, nelems);
+}
+
+#define ISHMEMI_CXX_COLL_TYPED(TYPENAME, TYPE, UNUSED1, UNUSED2)                                    \
+    inline int ishmem_##TYPENAME##_fcollect(TYPE *d, const TYPE *s, size_t n) { return ishmem_fcollect(d, s, n); } \
+    inline int ishmem_##TYPENAME##_fcollect(ishmem_team_t t, TYPE *d, const TYPE *s, size_t n)     \
+    {                                                                                              \
+        return ishmem_fcollect(t, d, s, n);                                                        \
+    }                                                                                              \
+    inline int ishmem_##TYPENAME##_collect(TYPE *d, const TYPE *s, size_t n) { return ishmem_collect(d, s, n); } \
+    inline int ishmem_##TYPENAME##_collect(ishmem_team_t t, TYPE *d, const TYPE *s, size_t n)      \
+    {                                                                                              \
+        return ishmem_collect(t, d, s, n);                                                         \
+    }                                                                                              \
+    inline int ishmem_##TYPENAME##_sum_inscan(TYPE *d, const TYPE *s, size_t n) { return ishmem_sum_inscan(d, s, n); } \
+    inline int ishmem_##TYPENAME##_sum_inscan(ishmem_team_t t, TYPE *d, const TYPE *s, size_t n)   \
+    {                                                                                              \
+        return ishmem_sum_inscan(t, d, s, n);                                                      \
+    }                                                                                              \
+    inline int ishmem_##TYPENAME##_sum_exscan(TYPE *d, const TYPE *s, size_t n) { return ishmem_sum_exscan(d, s, n); } \
+    inline int ishmem_##TYPENAME##_sum_exscan(ishmem_team_t t, TYPE *d, const TYPE *s, size_t n)   \
+    {                                                                                              \
+        return ishmem_sum_exscan(t, d, s, n);                                                      \
+    }
+
+/* fcollect / collect / inscan / exscan typename lists = src/collectives/collect.cpp:44-66,
+ * :129-151 and scan.cpp:28-74: the same 23 names as max/min/sum/prod. */
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_COLL_TYPED, _, _)
+
 #endif /* ISHMEM_AMD_ISHMEM_H */

@@ -129,6 +129,23 @@ int ishmemi_c_reduce_on_stream(int team, int op, int dtype, void *dest, const vo
 int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n,
                       void *stream);
 
+/* ---- the collectives next to the reduce, same machinery -------------
+ * fcollect: dest[j*nbytes ..] = member j's source, in team order, on every member
+ *   (ishmem_<TN>_fcollect / ishmem_fcollectmem, src/ishmem.h:894-921, collect_impl.h).
+ * collect: members may contribute different byte counts; concatenated in team order
+ *   (ishmem_<TN>_collect / ishmem_collectmem).  Blocking only.
+ * scan: prefix sum over the team in team order, inclusive (ishmem_<TN>_sum_inscan) or exclusive
+ *   (ishmem_<TN>_sum_exscan; the first member gets 0), src/collectives/scan_impl.h, proxied by the
+ *   reference to MPI_Scan / MPI_Exscan (src/runtime/runtime_mpi.cpp:816-835).
+ * For teams of more than one PE, source and dest must be symmetric-heap memory. */
+int ishmemi_c_fcollect(int team, void *dest, const void *source, size_t nbytes);
+int ishmemi_c_fcollect_on_stream(int team, void *dest, const void *source, size_t nbytes, int *ret,
+                                 void *stream);
+int ishmemi_c_collect(int team, void *dest, const void *source, size_t nbytes);
+int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *source, size_t nelems);
+int ishmemi_c_scan_on_stream(int team, int dtype, int inclusive, void *dest, const void *source,
+                             size_t nelems, int *ret, void *stream);
+
 /* ---- device-initiated collectives ----------------------------------------------------------
  * The reference's device-callable reductions (ishmemx_<TN>_<op>_reduce_work_group,
  * src/collectives/reduce_impl.h:386-418, :505-518, src/ishmemx.h:1648-1699) read the library

@@ -217,7 +217,51 @@ def _make_on_stream(op: str, dt: str):
     return fn
 
 
+# ---- fcollect / collect / scan (src/collectives/collect.cpp, scan.cpp) --
+def ishmem_fcollectmem(*args) -> int:
+    """ishmem_fcollectmem([team,] dest, source, nbytes) -> int (bytes per PE)."""
+    team, (dest, source, n) = (ISHMEM_TEAM_WORLD, args) if len(args) == 3 else (args[0], args[1:])
+    return _L.ishmemi_c_fcollect(team, dest, source, n)
+
+
+def ishmem_collectmem(*args) -> int:
+    """ishmem_collectmem([team,] dest, source, nbytes) -> int (nbytes may differ per PE)."""
+    team, (dest, source, n) = (ISHMEM_TEAM_WORLD, args) if len(args) == 3 else (args[0], args[1:])
+    return _L.ishmemi_c_collect(team, dest, source, n)
+
+
+def fcollect_on_stream(dest: int, source: int, nbytes: int, ret: int | None, stream: int,
+                       team: int = ISHMEM_TEAM_WORLD) -> int:
+    return _L.ishmemi_c_fcollect_on_stream(team, dest, source, nbytes, ret or None, stream or None)
+
+
+def scan(dtype: str, inclusive: bool, dest: int, source: int, nelems: int,
+         team: int = ISHMEM_TEAM_WORLD) -> int:
+    return _L.ishmemi_c_scan(team, DTYPES[dtype], 1 if inclusive else 0, dest, source, nelems)
+
+
+def _make_coll(kind: str, dt: str, size: int):
+    def fn(*args):
+        team, (dest, source, n) = (ISHMEM_TEAM_WORLD, args) if len(args) == 3 else (args[0], args[1:])
+        if kind == "fcollect":
+            return _L.ishmemi_c_fcollect(team, dest, source, n * size)
+        if kind == "collect":
+            return _L.ishmemi_c_collect(team, dest, source, n * size)
+        return _L.ishmemi_c_scan(team, DTYPES[dt], 1 if kind == "inscan" else 0, dest, source, n)
+    return fn
+
+
+_SIZES = {"int8": 1, "uint8": 1, "int16": 2, "uint16": 2, "int32": 4, "uint32": 4, "float": 4,
+          "int64": 8, "uint64": 8, "double": 8}
+
 _mod = sys.modules[__name__]
+for _tn in ARITH_TYPENAMES:  # the reference's fcollect / collect / scan lists = these 23 names
+    for _kind, _name in (("fcollect", f"ishmem_{_tn}_fcollect"), ("collect", f"ishmem_{_tn}_collect"),
+                         ("inscan", f"ishmem_{_tn}_sum_inscan"), ("exscan", f"ishmem_{_tn}_sum_exscan")):
+        _f = _make_coll(_kind, TYPENAMES[_tn], _SIZES[TYPENAMES[_tn]])
+        _f.__name__ = _name
+        setattr(_mod, _name, _f)
+del _tn, _kind, _name, _f
 API_NAMES: list[str] = []
 for _op, _tns in TYPENAMES_FOR_OP.items():
     for _tn in _tns:

@@ -21,7 +21,7 @@ LIB = PKG / "libishmem_amd.so"
 # (source, object stem, extra flags): kernels_op.hip is compiled once per reduction op so the
 # ~350 kernel instantiations build in parallel.
 SOURCES = [("kernels.hip", "kernels", []), ("runtime.cpp", "runtime", []),
-           ("bootstrap.cpp", "bootstrap", [])] + [
+           ("bootstrap.cpp", "bootstrap", []), ("kernels_coll.hip", "kernels_coll", [])] + [
     ("kernels_op.hip", f"kernels_op{op}", [f"-DISHMEMI_KOP={op}"]) for op in range(7)]
 ARCH = os.environ.get("ISHMEM_OFFLOAD_ARCH", "gfx950")
 

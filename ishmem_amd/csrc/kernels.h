@@ -62,6 +62,41 @@ struct LLArgs {
 };
 hipError_t launch_ll(int op, int dt, const LLArgs &a, hipStream_t s);
 
+// fcollect / collect (all-gather of the members' sources): member j's bytes land at
+// dst + dst_off[j].  Same pairwise barriers as the reduce (start, end).
+struct CollectArgs {
+    const char *src[kMaxPes];  // member j's source, mapped here
+    char *dst;
+    uint64_t dst_off[kMaxPes];
+    uint64_t nbytes[kMaxPes];
+    uint32_t *my_flags;
+    uint32_t *peer_flags[kMaxPes];
+    uint32_t *err;
+    int *ret;
+    uint64_t timeout_ticks;
+    uint32_t epoch;
+    int p, me;
+    int unit;  // bytes per item: 16, 4 or 1 (largest dividing every address and length)
+};
+hipError_t launch_collect(const CollectArgs &a, int grid, hipStream_t s);
+
+// Inclusive / exclusive prefix sum across the team (MPI_Scan / MPI_Exscan semantics).
+struct ScanArgs {
+    const char *src[kMaxPes];      // member j's source
+    const char *scratch[kMaxPes];  // member j's scratch (staging region), mapped here
+    char *dst;
+    uint32_t *my_flags;
+    uint32_t *peer_flags[kMaxPes];
+    uint32_t *err;
+    int *ret;
+    uint64_t nelems, items_per_chunk;
+    uint64_t timeout_ticks;
+    uint32_t epoch;
+    int p, me;
+    int inclusive;
+};
+hipError_t launch_scan(int dt, const ScanArgs &a, int grid, hipStream_t s);
+
 // Arguments of the local k-input fan-in combine: dst = op(src0, src1, ..., src_{k-1}).
 constexpr int kMaxFanin = 16;
 struct FaninArgs {

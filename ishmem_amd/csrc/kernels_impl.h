@@ -151,8 +151,8 @@ __device__ __forceinline__ uint32_t *flag_slot(uint32_t *base, int phase, int bl
 // its own slot of every peer's flag row, then polls its local row until every peer's slot
 // holds the epoch (wrap-safe compare).  Called by ALL threads of the block; returns false on
 // timeout (recorded in *err) so the caller can drain instead of hanging the GPU.
-template <bool RELEASE>
-__device__ bool pe_barrier(const ReduceArgs &a, int phase, int block)
+template <bool RELEASE, typename A>
+__device__ bool pe_barrier(const A &a, int phase, int block)
 {
     __shared__ int s_ok;
     // Every storing wave drains its stores, then one wave publishes (Guideline 16, R1).

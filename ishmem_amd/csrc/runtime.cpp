@@ -430,6 +430,131 @@ int reduce_staged(State &s, int team, int op, int dt, void *dst, const void *src
     return 0;
 }
 
+// ---------------- fcollect / collect / scan --------------------------
+int team_sync_locked(State &s, int team, hipStream_t st, int *ret);
+
+template <typename A>
+int fill_team_sync_args(State &s, int team, A &a, std::string &why)
+{
+    ReduceArgs r;
+    if (team_args(s, team, r, why)) return 1;
+    a.my_flags = r.my_flags;
+    for (int j = 0; j < r.p; ++j) a.peer_flags[j] = r.peer_flags[j];
+    a.err = r.err;
+    a.timeout_ticks = r.timeout_ticks;
+    a.epoch = r.epoch;
+    a.p = r.p;
+    a.me = r.me;
+    return 0;
+}
+
+// nbytes[j] = bytes member j contributes; dest slot of j starts at the sum of the earlier ones.
+int collect_launch(State &s, int team, void *dst, const void *src, const uint64_t *nbytes, int *ret,
+                   hipStream_t st)
+{
+    Team &t = s.teams[team];
+    CollectArgs a;
+    memset(&a, 0, sizeof(a));
+    std::string why;
+    if (fill_team_sync_args(s, team, a, why)) return fail("collect: " + why);
+    uint64_t off = 0, orv = (uintptr_t) src | (uintptr_t) dst, maxb = 0;
+    for (int j = 0; j < t.size; ++j) {
+        const int gpe = t.start + j * t.stride;
+        a.src[j] = translate(s, src, gpe);
+        if (!a.src[j]) return fail("collect: source must be symmetric-heap memory");
+        a.dst_off[j] = off;
+        a.nbytes[j] = nbytes[j];
+        orv |= off | nbytes[j];
+        off += nbytes[j];
+        maxb = std::max(maxb, nbytes[j]);
+    }
+    a.dst = (char *) dst;
+    a.ret = ret;
+    a.unit = (orv & 15) == 0 ? 16 : (orv & 3) == 0 ? 4 : 1;
+    const uint64_t items = maxb / a.unit, tile = (uint64_t) kBlock * kUnroll;
+    const int grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((items + tile - 1) / tile, s.max_blocks));
+    HIP_TRY(launch_collect(a, grid, st));
+    return 0;
+}
+
+int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret, hipStream_t st,
+                  bool blocking)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.initialized) return fail("fcollect: not initialized");
+    if (team < 0 || team >= kMaxTeams || !s.teams[team].valid || s.teams[team].my_idx < 0)
+        return fail("fcollect: invalid team or caller not a member");
+    Team &t = s.teams[team];
+    if (t.size == 1) {
+        if (nbytes && dst != src && launch_copy(dst, src, nbytes, st)) return 1;
+        if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
+    } else {
+        if (!in_heap(s, dst)) return fail("fcollect: dest must be symmetric-heap memory");
+        uint64_t nb[kMaxPes];
+        for (int j = 0; j < t.size; ++j) nb[j] = nbytes;
+        if (collect_launch(s, team, dst, src, nb, ret, st)) return 1;
+    }
+    if (blocking) {
+        HIP_TRY(hipStreamSynchronize(st));
+        if (check_team_errors(s, team)) return 1;
+    }
+    return 0;
+}
+
+int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_t n, int *ret,
+              hipStream_t st, bool blocking)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.initialized) return fail("scan: not initialized");
+    if (!op_dtype_valid(ISHMEMI_OP_SUM, dt)) return fail("scan: invalid dtype");
+    if (team < 0 || team >= kMaxTeams || !s.teams[team].valid || s.teams[team].my_idx < 0)
+        return fail("scan: invalid team or caller not a member");
+    Team &t = s.teams[team];
+    const size_t es = dtype_size(dt);
+    if (t.size == 1) {  // inclusive: the source; exclusive: the sum of nothing
+        if (n && inclusive && dst != src && launch_copy(dst, src, n * es, st)) return 1;
+        if (n && !inclusive) HIP_TRY(hipMemsetAsync(dst, 0, n * es, st));
+        if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
+    } else if (n == 0) {
+        if (team_sync_locked(s, team, st, ret)) return 1;
+    } else {
+        if (!in_heap(s, dst) || !in_heap(s, src)) return fail("scan: buffers must be symmetric-heap memory");
+        if (((uintptr_t) dst | (uintptr_t) src) % es) return fail("scan: misaligned buffers");
+        // Segments whose p scratch rows fit the staging region (member c's rows: [k][chunk c]).
+        const uint64_t ipc_max = ((s.staging_bytes / es) / (uint64_t) t.size) & ~uint64_t(63);
+        const uint64_t seg = ipc_max * (uint64_t) t.size;
+        if (ipc_max == 0) return fail("scan: staging region too small for this team");
+        for (uint64_t off = 0; off < n; off += seg) {
+            const uint64_t m = std::min<uint64_t>(seg, n - off);
+            ScanArgs a;
+            memset(&a, 0, sizeof(a));
+            std::string why;
+            if (fill_team_sync_args(s, team, a, why)) return fail("scan: " + why);
+            for (int j = 0; j < t.size; ++j) {
+                const int gpe = t.start + j * t.stride;
+                a.src[j] = translate(s, (const char *) src + off * es, gpe);
+                a.scratch[j] = translate(s, s.staging, gpe);
+            }
+            a.dst = (char *) dst + off * es;
+            a.ret = ret;
+            a.nelems = m;
+            a.items_per_chunk = items_per_chunk(m, t.size);
+            a.inclusive = inclusive;
+            const uint64_t tile = (uint64_t) kBlock * kUnroll;
+            const int grid = (int) std::max<uint64_t>(
+                1, std::min<uint64_t>((a.items_per_chunk + tile - 1) / tile, s.max_blocks));
+            HIP_TRY(launch_scan(dt, a, grid, st));
+        }
+    }
+    if (blocking) {
+        HIP_TRY(hipStreamSynchronize(st));
+        if (check_team_errors(s, team)) return 1;
+    }
+    return 0;
+}
+
 int team_sync_locked(State &s, int team, hipStream_t st, int *ret)
 {
     Team &t = s.teams[team];
@@ -590,7 +715,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             // Uncached allocations that cannot be exported: fall back to coarse-grained flags
             // (every flag access is a system-scope atomic, so correctness does not depend on it).
             (void) hipGetLastError();
-            hipFree(s.flags);
+            (void) hipFree(s.flags);
             HIP_TRY(hipMalloc((void **) &s.flags, flag_bytes));
             HIP_TRY(hipMemset(s.flags, 0, flag_bytes));
             HIP_TRY(hipDeviceSynchronize());
@@ -693,14 +818,14 @@ int ishmemi_c_finalize(void)
     State &s = S();
     std::lock_guard<std::mutex> lk(s.mu);
     if (!s.initialized) return 0;
-    hipDeviceSynchronize();
+    (void) hipDeviceSynchronize();
     if (s.npes > 1) {
         std::string err;
         s.boot.barrier(err);  // no peer may still be reading our heap
         for (int j = 0; j < s.npes; ++j) {
             if (j == s.pe) continue;
-            if (s.peer_heap[j]) hipIpcCloseMemHandle(s.peer_heap[j]);
-            if (s.peer_flags[j]) hipIpcCloseMemHandle(s.peer_flags[j]);
+            if (s.peer_heap[j]) (void) hipIpcCloseMemHandle(s.peer_heap[j]);
+            if (s.peer_flags[j]) (void) hipIpcCloseMemHandle(s.peer_flags[j]);
             s.peer_heap[j] = nullptr;
             s.peer_flags[j] = nullptr;
         }
@@ -708,20 +833,20 @@ int ishmemi_c_finalize(void)
         s.boot.detach();
     }
     if (s.copy_in) {
-        hipStreamDestroy(s.copy_in);
-        hipStreamDestroy(s.copy_out);
+        (void) hipStreamDestroy(s.copy_in);
+        (void) hipStreamDestroy(s.copy_out);
         for (int i = 0; i < 2; ++i) {
-            hipEventDestroy(s.ev_in[i]);
-            hipEventDestroy(s.ev_red[i]);
-            hipEventDestroy(s.ev_out[i]);
+            (void) hipEventDestroy(s.ev_in[i]);
+            (void) hipEventDestroy(s.ev_red[i]);
+            (void) hipEventDestroy(s.ev_out[i]);
         }
         s.copy_in = s.copy_out = nullptr;
     }
-    hipFree(s.heap);
-    hipFree(s.flags);
-    hipHostFree(s.err_host);
-    hipFree(s.dctx);
-    hipFree(s.dev_epochs);
+    (void) hipFree(s.heap);
+    (void) hipFree(s.flags);
+    (void) hipHostFree(s.err_host);
+    (void) hipFree(s.dctx);
+    (void) hipFree(s.dev_epochs);
     s.dctx = nullptr;
     s.dev_epochs = nullptr;
     s.heap = nullptr;
@@ -776,7 +901,7 @@ void ishmemi_c_free(void *ptr)
 {
     State &s = S();
     if (!s.initialized) return;
-    hipDeviceSynchronize();
+    (void) hipDeviceSynchronize();
     if (s.npes > 1) {  // src/memory.cpp:286: peers must be done with the buffer
         std::string err;
         s.boot.barrier(err);
@@ -989,6 +1114,52 @@ int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int
     f.tail = pl.tail;
     HIP_TRY(launch_fanin(op, dtype, pl.vec, f, pl.grid, (hipStream_t) stream));
     return 0;
+}
+
+int ishmemi_c_fcollect(int team, void *dest, const void *source, size_t nbytes)
+{
+    return fcollect_impl(team, dest, source, nbytes, nullptr, 0, true);
+}
+
+int ishmemi_c_fcollect_on_stream(int team, void *dest, const void *source, size_t nbytes, int *ret,
+                                 void *stream)
+{
+    return fcollect_impl(team, dest, source, nbytes, ret, (hipStream_t) stream, false);
+}
+
+int ishmemi_c_collect(int team, void *dest, const void *source, size_t nbytes)
+{
+    // Every member's byte count first (an fcollect of one u64 through the team scratch), then
+    // the all-gather at the resulting offsets (src/collectives/collect_impl.h:36-50).
+    State &s = S();
+    if (!s.initialized) return fail("collect: not initialized");
+    if (team < 0 || team >= kMaxTeams || !s.teams[team].valid || s.teams[team].my_idx < 0)
+        return fail("collect: invalid team or caller not a member");
+    const int p = s.teams[team].size;
+    if (p == 1) return ishmemi_c_fcollect(team, dest, source, nbytes);
+    const uint64_t mine = nbytes;
+    if (hipMemcpy(s.team_scratch, &mine, 8, hipMemcpyHostToDevice) != hipSuccess)
+        return fail("collect: count copy failed");
+    if (ishmemi_c_fcollect(team, s.team_scratch + 64, s.team_scratch, 8)) return 1;
+    uint64_t counts[kMaxPes];
+    if (hipMemcpy(counts, s.team_scratch + 64, 8 * (size_t) p, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail("collect: count copy failed");
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!in_heap(s, dest)) return fail("collect: dest must be symmetric-heap memory");
+    if (collect_launch(s, team, dest, source, counts, nullptr, 0)) return 1;
+    HIP_TRY(hipStreamSynchronize(0));
+    return check_team_errors(s, team);
+}
+
+int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *source, size_t nelems)
+{
+    return scan_impl(team, dtype, inclusive, dest, source, nelems, nullptr, 0, true);
+}
+
+int ishmemi_c_scan_on_stream(int team, int dtype, int inclusive, void *dest, const void *source,
+                             size_t nelems, int *ret, void *stream)
+{
+    return scan_impl(team, dtype, inclusive, dest, source, nelems, ret, (hipStream_t) stream, false);
 }
 
 void *ishmemi_c_device_ctx(void)

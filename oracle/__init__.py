@@ -128,3 +128,53 @@ def fp_tolerance(dt: int, op: int, srcs: list[np.ndarray], ref: np.ndarray) -> n
     if op == OPS["prod"]:
         return (p - 1) * u * np.abs(ref.astype(np.float64)) * 1.0001 + np.finfo(np.float64).tiny
     return np.zeros(ref.shape)
+
+
+# ---- fcollect / collect / scan ----------------------------------------
+def scan_fold(dt: int, srcs: list[np.ndarray], me: int, inclusive: bool) -> np.ndarray:
+    """Team-order prefix sum for PE `me`: the proxy hands the request to MPI_Scan / MPI_Exscan
+    with MPI_SUM (src/runtime/runtime_mpi.cpp:815-835); integers wrap (two's complement), floats
+    fold linearly x0+x1+...  Exscan on the first PE yields 0 (test/unit/exscan.cpp:52 checks 0)."""
+    t = NP[dt]
+    out = np.zeros_like(np.asarray(srcs[0], dtype=t))
+    last = me + 1 if inclusive else me
+    with np.errstate(over="ignore"):
+        for k in range(last):
+            out = np.asarray(srcs[k], dtype=t).copy() if k == 0 else (out + np.asarray(srcs[k], dtype=t)).astype(t)
+    return out
+
+
+def _words(nbytes: int) -> np.ndarray:
+    return np.arange(nbytes // 8 + 1, dtype=np.int64)
+
+
+def scan_pattern_source(pe: int, nbytes: int) -> np.ndarray:
+    """test/unit/inscan.cpp / exscan.cpp:30-43: long word idx = pe + idx; first nbytes bytes."""
+    w = (pe + _words(nbytes)).astype(np.int64)
+    return w.view(np.uint8)[:nbytes].copy()
+
+
+def scan_pattern_check(pe: int, nbytes: int, inclusive: bool) -> np.ndarray:
+    """inscan.cpp:46-58 ((pe+i)(pe+i+1)/2 - i(i-1)/2) and exscan.cpp:46-59 ((pe+i)(pe+i-1)/2 -
+    i(i-1)/2), evaluated on 64-bit words like the tester."""
+    i = _words(nbytes)
+    a = pe + i
+    w = (a * (a + 1) // 2 if inclusive else a * (a - 1) // 2) - (i * (i - 1)) // 2
+    return w.astype(np.int64).view(np.uint8)[:nbytes].copy()
+
+
+def collect_pattern_source(pe: int, nelems: int, elem_size: int) -> np.ndarray:
+    """test/unit/fcollect.cpp:48-62 / collect.cpp:68-82: word idx =
+    (nelems<<48) + ((0x80+pe)<<40) + (0xff<<32) + idx; first nelems*elem_size bytes."""
+    nbytes = nelems * elem_size
+    i = _words(nbytes).astype(np.uint64)
+    w = (np.uint64(nelems) << np.uint64(48)) + (np.uint64(0x80 + pe) << np.uint64(40)) + \
+        (np.uint64(0xff) << np.uint64(32)) + i
+    return w.view(np.uint8)[:nbytes].copy()
+
+
+def collect_check(counts: list[int], elem_size: int) -> np.ndarray:
+    """test/unit/collect.cpp:85-107 (fcollect.cpp the equal-count case): the members' source
+    patterns concatenated in team order."""
+    return np.concatenate([collect_pattern_source(pe, c, elem_size) for pe, c in enumerate(counts)]
+                          + [np.zeros(0, np.uint8)])

@@ -275,6 +275,113 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             ish.ishmem_free(d_base)
             ish.ishmem_free(s_base)
 
+        if "collect" in scenarios:
+            # fcollect.cpp / collect.cpp testers: per-PE word pattern, dest = the members' blocks
+            # concatenated in team order; offsets 0..14 in steps of sizeof(T) like
+            # collect.cpp:109-141; collect counts drawn per PE (collect.cpp:120-124).
+            rng = np.random.default_rng(4242)
+            for tn, es in (("uchar", 1), ("short", 2), ("float", 4), ("double", 8)):
+                for nelems in (1, 3, 1000, 40_001):
+                    counts_c = [int(c) for c in rng.integers(1, nelems + 1, npes)]
+                    for so, do in ((0, 0), (es, 3 * es), (7 * es if es < 2 else 2 * es, 0)):
+                        src_b = ish.ishmem_malloc(nelems * es + 64)
+                        dst_b = ish.ishmem_malloc(npes * nelems * es + 64)
+                        hip.upload(src_b + so, oracle.collect_pattern_source(pe, nelems, es))
+                        fn = getattr(ish, f"ishmem_{tn}_fcollect")
+                        r = fn(dst_b + do, src_b + so, nelems)
+                        want = oracle.collect_check([nelems] * npes, es)
+                        if r:
+                            fails.append(f"pe{pe} fcollect {tn} n{nelems} rc={r} {ish.last_error()}")
+                        elif not _bits_equal(hip.download(dst_b + do, want.size, np.uint8), want):
+                            fails.append(f"pe{pe} fcollect {tn} n{nelems} so{so} do{do} wrong")
+                        c = counts_c[pe]
+                        hip.upload(src_b + so, oracle.collect_pattern_source(pe, c, es))
+                        r = getattr(ish, f"ishmem_{tn}_collect")(dst_b + do, src_b + so, c)
+                        want = oracle.collect_check(counts_c, es)
+                        if r:
+                            fails.append(f"pe{pe} collect {tn} rc={r} {ish.last_error()}")
+                        elif not _bits_equal(hip.download(dst_b + do, want.size, np.uint8), want):
+                            fails.append(f"pe{pe} collect {tn} counts{counts_c} so{so} do{do} wrong")
+                        ish.ishmem_free(dst_b)
+                        ish.ishmem_free(src_b)
+            # fcollectmem of odd byte counts; nelems 0 (still a team sync)
+            src_b, dst_b = ish.ishmem_malloc(4096), ish.ishmem_malloc(4096 * npes)
+            hip.upload(src_b, oracle.collect_pattern_source(pe, 1001, 1))
+            if ish.ishmem_fcollectmem(dst_b, src_b, 1001) or not _bits_equal(
+                    hip.download(dst_b, 1001 * npes, np.uint8), oracle.collect_check([1001] * npes, 1)):
+                fails.append(f"pe{pe} fcollectmem 1001 B wrong {ish.last_error()}")
+            if ish.ishmem_int_fcollect(dst_b, src_b, 0) or ish.ishmem_collectmem(dst_b, src_b, 0):
+                fails.append(f"pe{pe} fcollect n=0 failed {ish.last_error()}")
+            # on a strided team (even PEs) via the team overload
+            if npes >= 2:
+                r, team = ish.ishmem_team_split_strided(ish.ISHMEM_TEAM_WORLD, 0, 2, (npes + 1) // 2)
+                if team != ish.ISHMEM_TEAM_INVALID:
+                    members = list(range(0, npes, 2))
+                    hip.upload(src_b, oracle.collect_pattern_source(members.index(pe), 333, 4))
+                    want = oracle.collect_check([333] * len(members), 4)
+                    if ish.ishmem_int32_fcollect(team, dst_b, src_b, 333) or not _bits_equal(
+                            hip.download(dst_b, want.size, np.uint8), want):
+                        fails.append(f"pe{pe} team fcollect wrong {ish.last_error()}")
+                    ish.ishmem_team_destroy(team)
+            ish.ishmem_free(dst_b)
+            ish.ishmem_free(src_b)
+
+        if "scan" in scenarios:
+            # inscan.cpp / exscan.cpp testers (word pattern pe+idx, closed-form check) over the
+            # reference's scan_types, then seeded random inputs vs the oracle's team-order fold.
+            for tn in ("short", "int", "long", "ushort", "uint", "size", "int16", "uint64", "float", "double"):
+                dt = DT[ish.TYPENAMES[tn]]
+                es = np.dtype(oracle.NP[dt]).itemsize
+                for nelems in (1, 5, 4096 + 3, 70_001):
+                    nb = nelems * es
+                    s_b, d_b = ish.ishmem_malloc(nb + 64), ish.ishmem_malloc(nb + 64)
+                    hip.upload(s_b, oracle.scan_pattern_source(pe, nb))
+                    for inc in (True, False):
+                        fn = getattr(ish, f"ishmem_{tn}_sum_{'inscan' if inc else 'exscan'}")
+                        hip.memset(d_b, 0xA5, nb)
+                        r = fn(d_b, s_b, nelems)
+                        if r:
+                            fails.append(f"pe{pe} {tn} scan rc={r} {ish.last_error()}")
+                            continue
+                        got = hip.download(d_b, nb, np.uint8)
+                        srcs = [oracle.scan_pattern_source(j, nb).view(oracle.NP[dt]) for j in range(npes)]
+                        if not _bits_equal(got, oracle.scan_fold(dt, srcs, pe, inc)):
+                            fails.append(f"pe{pe} {tn} {'in' if inc else 'ex'}scan n{nelems} != oracle")
+                        # The tester's closed form holds while no lane carries (its word sums
+                        # stay below 2^(8*sizeof T)); beyond that the oracle above is the check.
+                        if nelems <= 4099 and not _bits_equal(got, oracle.scan_pattern_check(pe, nb, inc)):
+                            fails.append(f"pe{pe} {tn} {'in' if inc else 'ex'}scan n{nelems} != tester check pattern")
+                    ish.ishmem_free(d_b)
+                    ish.ishmem_free(s_b)
+            for dt in (DT["int8"], DT["int32"], DT["uint64"], DT["float"], DT["double"]):
+                n = 123_457
+                ins = [oracle.fill_random(dt, 600 + j, n) for j in range(npes)]
+                if dt >= 8:
+                    ins[0][:3] = -0.0  # first term passes through unchanged (sign of zero kept)
+                s_b, d_b = heap(n, dt), heap(n, dt)
+                hip.upload(s_b, ins[pe])
+                for inc in (True, False):
+                    r = ish.scan(NAMES[dt], inc, d_b, s_b, n)
+                    ref = oracle.scan_fold(dt, ins, pe, inc)
+                    got = hip.download(d_b, n, oracle.NP[dt])
+                    if r:
+                        fails.append(f"pe{pe} scan dt{dt} rc={r} {ish.last_error()}")
+                    elif not _bits_equal(got, ref):
+                        fails.append(f"pe{pe} scan dt{dt} inc={inc}: "
+                                     f"{int(np.sum(got.view(np.uint8) != ref.view(np.uint8)))} bytes differ")
+                ish.ishmem_free(d_b)
+                ish.ishmem_free(s_b)
+            # several staging-sized segments (ISHMEM_STAGING_SIZE small in the test env)
+            n = 3 * (ish.get_param("staging_bytes") // 4) + 17
+            ins = [oracle.fill_random(DT["int32"], 700 + j, n) for j in range(npes)]
+            s_b, d_b = heap(n, DT["int32"]), heap(n, DT["int32"])
+            hip.upload(s_b, ins[pe])
+            if ish.ishmem_int32_sum_inscan(d_b, s_b, n) or not _bits_equal(
+                    hip.download(d_b, n, np.int32), oracle.scan_fold(DT["int32"], ins, pe, True)):
+                fails.append(f"pe{pe} multi-segment scan wrong {ish.last_error()}")
+            ish.ishmem_free(d_b)
+            ish.ishmem_free(s_b)
+
         if ish.lib().ishmemi_c_error_count() != 0:
             fails.append(f"pe{pe} device barrier timeouts: {ish.lib().ishmemi_c_error_count()}")
         ish.ishmem_barrier_all()

@@ -64,3 +64,9 @@ def test_large_f32_sum_256MiB_per_pe():
 
 def test_huge_2p5GiB_per_pe_head_tail_and_2GiB_boundary():
     run_pes(2, ["huge"], env={"ISHMEM_MAX_BLOCKS": 64, "ISHMEM_SYMMETRIC_SIZE": "6G"}, timeout=400)
+
+
+@pytest.mark.parametrize("npes", [2, 3, 4])
+def test_fcollect_collect_scan_vs_tester_patterns_and_oracle(npes):
+    # Small staging region so the scan's segment loop runs several times.
+    run_pes(npes, ["collect", "scan"], env={"ISHMEM_STAGING_SIZE": "4M"}, timeout=300)

@@ -114,3 +114,25 @@ def test_long_reduce_known_answer():
 def test_host_proxy_timer_runs():
     t = oracle.host_proxy_time(oracle.OPS["sum"], oracle.DTYPES["int32"], 1 << 16, 2, 2)
     assert 0 < t < 10
+
+
+def test_scan_fold_reproduces_reference_tester_check_patterns():
+    # inscan.cpp:46-58 / exscan.cpp:46-59 closed forms vs the oracle's team-order prefix fold on
+    # the testers' source pattern, for every dtype (FP words are exact denormal sums).
+    for dt in range(10):
+        es = np.dtype(oracle.NP[dt]).itemsize
+        for p in (1, 2, 3, 4, 8):
+            for nb in (es, 8 * es, 41 * es):
+                srcs = [oracle.scan_pattern_source(pe, nb).view(oracle.NP[dt]) for pe in range(p)]
+                for me in range(p):
+                    for inc in (True, False):
+                        got = oracle.scan_fold(dt, srcs, me, inc).view(np.uint8)
+                        assert np.array_equal(got, oracle.scan_pattern_check(me, nb, inc)), (dt, p, nb, me, inc)
+
+
+def test_collect_check_is_concatenation_of_sources():
+    src = [oracle.collect_pattern_source(pe, c, 2) for pe, c in enumerate([3, 1, 5])]
+    chk = oracle.collect_check([3, 1, 5], 2)
+    assert np.array_equal(chk, np.concatenate(src))
+    w = oracle.collect_pattern_source(1, 4, 8).view(np.uint64)
+    assert int(w[2]) == (4 << 48) + (0x81 << 40) + (0xff << 32) + 2  # fcollect.cpp:54-55
