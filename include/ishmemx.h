@@ -49,6 +49,63 @@ ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, min, ISHMEMI_OP_MIN)
 ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, sum, ISHMEMI_OP_SUM)
 ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, prod, ISHMEMI_OP_PROD)
 
+/* fcollect / scan on a stream (src/ishmemx.h fcollect/inscan/exscan _on_queue). */
+inline int ishmemx_fcollectmem_on_stream(ishmem_team_t team, void *dest, const void *source,
+                                         size_t nbytes, int *ret, hipStream_t stream)
+{
+    return ishmemi_c_fcollect_on_stream(team, dest, source, nbytes, ret, (void *) stream);
+}
+inline int ishmemx_fcollectmem_on_stream(void *dest, const void *source, size_t nbytes, int *ret,
+                                         hipStream_t stream)
+{
+    return ishmemx_fcollectmem_on_stream(ISHMEM_TEAM_WORLD, dest, source, nbytes, ret, stream);
+}
+
+#define ISHMEMI_CXX_COLL_ON_STREAM(TYPENAME, TYPE, UNUSED1, UNUSED2)                                 \
+    inline int ishmemx_##TYPENAME##_fcollect_on_stream(ishmem_team_t team, TYPE *dest,              \
+                                                       const TYPE *source, size_t nelems, int *ret, \
+                                                       hipStream_t stream)                          \
+    {                                                                                              \
+        return ishmemi_c_fcollect_on_stream(team, (void *) dest, (const void *) source,             \
+                                            nelems * sizeof(TYPE), ret, (void *) stream);           \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_fcollect_on_stream(TYPE *dest, const TYPE *source,              \
+                                                       size_t nelems, int *ret, hipStream_t stream) \
+    {                                                                                              \
+        return ishmemx_##TYPENAME##_fcollect_on_stream(ISHMEM_TEAM_WORLD, dest, source, nelems,    \
+                                                       ret, stream);                               \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_sum_inscan_on_stream(ishmem_team_t team, TYPE *dest,            \
+                                                         const TYPE *source, size_t nelems,         \
+                                                         int *ret, hipStream_t stream)              \
+    {                                                                                              \
+        return ishmemi_c_scan_on_stream(team, ishmemi_cxx::dtype_of<TYPE>(), 1, (void *) dest,      \
+                                        (const void *) source, nelems, ret, (void *) stream);       \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_sum_inscan_on_stream(TYPE *dest, const TYPE *source,            \
+                                                         size_t nelems, int *ret,                   \
+                                                         hipStream_t stream)                        \
+    {                                                                                              \
+        return ishmemx_##TYPENAME##_sum_inscan_on_stream(ISHMEM_TEAM_WORLD, dest, source, nelems,  \
+                                                         ret, stream);                             \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_sum_exscan_on_stream(ishmem_team_t team, TYPE *dest,            \
+                                                         const TYPE *source, size_t nelems,         \
+                                                         int *ret, hipStream_t stream)              \
+    {                                                                                              \
+        return ishmemi_c_scan_on_stream(team, ishmemi_cxx::dtype_of<TYPE>(), 0, (void *) dest,      \
+                                        (const void *) source, nelems, ret, (void *) stream);       \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_sum_exscan_on_stream(TYPE *dest, const TYPE *source,            \
+                                                         size_t nelems, int *ret,                   \
+                                                         hipStream_t stream)                        \
+    {                                                                                              \
+        return ishmemx_##TYPENAME##_sum_exscan_on_stream(ISHMEM_TEAM_WORLD, dest, source, nelems,  \
+                                                         ret, stream);                             \
+    }
+
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_COLL_ON_STREAM, _, _)
+
 /* Explicit-identity init (the role of ishmemx_init_attr, src/ishmemx.h:21-37). */
 inline int ishmemx_init_pe(int pe, int npes, int device, const char *bootstrap_key)
 {

@@ -120,6 +120,43 @@ int main()
         hipStreamDestroy(st);
         ishmem_free(ret);
     }
+    // fcollect (fcollect.cpp:48-62 pattern) and exscan on a stream (exscan.cpp:30-59 closed form).
+    {
+        const size_t n = 1000;
+        std::vector<long> src(n), got(n * npes);
+        for (size_t i = 0; i < n; ++i) src[i] = (long) (((long) n << 48) + ((0x80L + pe) << 40) + (0xffL << 32) + (long) i);
+        hipMemcpy(sb, src.data(), n * 8, hipMemcpyHostToDevice);
+        int r = ishmem_long_fcollect((long *) db, (const long *) sb, n);
+        hipMemcpy(got.data(), db, n * 8 * npes, hipMemcpyDeviceToHost);
+        for (int j = 0; j < npes && !r; ++j)
+            for (size_t i = 0; i < n; ++i)
+                if (got[j * n + i] != (long) (((long) n << 48) + ((0x80L + j) << 40) + (0xffL << 32) + (long) i)) r = -1;
+        if (r) {
+            ++errors;
+            printf("[%d] FAIL long_fcollect rc %d\n", pe, r);
+        }
+        for (size_t i = 0; i < n; ++i) src[i] = (long) pe + (long) i;
+        hipMemcpy(sb, src.data(), n * 8, hipMemcpyHostToDevice);
+        hipStream_t st;
+        hipStreamCreate(&st);
+        int *ret = (int *) ishmem_malloc(sizeof(int));
+        hipMemset(ret, 0xff, sizeof(int));
+        r = ishmemx_long_sum_exscan_on_stream((long *) db, (const long *) sb, n, ret, st);
+        hipStreamSynchronize(st);
+        int rv = -1;
+        hipMemcpy(&rv, ret, sizeof(int), hipMemcpyDeviceToHost);
+        hipMemcpy(got.data(), db, n * 8, hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < n && !r; ++i) {
+            const long a = pe + (long) i, ii = (long) i;
+            if (got[i] != a * (a - 1) / 2 - ii * (ii - 1) / 2) r = -1;
+        }
+        if (r || rv) {
+            ++errors;
+            printf("[%d] FAIL long_sum_exscan_on_stream rc %d ret %d\n", pe, r, rv);
+        }
+        hipStreamDestroy(st);
+        ishmem_free(ret);
+    }
     ishmem_free(db);
     ishmem_free(sb);
     ishmem_barrier_all();
