@@ -52,28 +52,36 @@ def pmc_traffic(kernel_tag: str, nbytes: int):
     return None
 
 
-def config5_sweep(ish, hip, src, dst, world, rank, dist, stream):
-    """min/max/prod x int32/float64, 4 KiB .. 64 MiB per PE: us per call (max over ranks), algbw."""
+def config5_sweep(ish, hip, src, dst, nbytes_max, world, rank, dist, stream):
+    """Config 5: min/max/prod x int32/float64, 4 KiB .. nbytes_max (the bench payload, 1 GiB by
+    default) per PE in steps of 4x: us per call (max over ranks), algbw, last 256 results checked
+    against the closed form of x_pe[i] = (i mod 1024) + pe."""
     import torch
     out = []
-    nbytes_max = 64 << 20
     for dtn, npd in (("int32", np.int32), ("double", np.float64)):
         es = np.dtype(npd).itemsize
         nmax = nbytes_max // es
         x = (np.arange(nmax, dtype=np.int64) % 1024).astype(npd) + npd(rank)
         hip.upload(src, x)
-        base = np.arange(nmax, dtype=np.int64) % 1024
-        for op in ("min", "max", "prod"):
+        del x
+
+        def expect(op, idx):
+            base = idx % 1024
             if op == "min":
-                exp_full = base.astype(npd)
-            elif op == "max":
-                exp_full = (base + world - 1).astype(npd)
-            else:
-                acc = base.astype(npd) if npd is np.float64 else base.astype(np.uint32)
+                return base.astype(npd)
+            if op == "max":
+                return (base + world - 1).astype(npd)
+            if npd is np.float64:
+                acc = base.astype(np.float64)
                 for pe in range(1, world):
-                    acc = acc * (base.astype(npd) + npd(pe)) if npd is np.float64 else \
-                        (acc * (base + pe).astype(np.uint32)).astype(np.uint32)
-                exp_full = acc.astype(npd) if npd is np.float64 else acc.view(np.int32)
+                    acc = acc * (base.astype(np.float64) + pe)
+                return acc
+            acc = base.astype(np.uint32)
+            for pe in range(1, world):
+                acc = (acc * (base + pe).astype(np.uint32)).astype(np.uint32)
+            return acc.view(np.int32)
+
+        for op in ("min", "max", "prod"):
             nb = 4096
             while nb <= nbytes_max:
                 n = nb // es
@@ -95,7 +103,8 @@ def config5_sweep(ish, hip, src, dst, world, rank, dist, stream):
                 us = float(t[0])
                 k = min(n, 256)
                 got = hip.download(dst + (n - k) * es, k, npd)
-                ok = bool(np.array_equal(got.view(np.uint8), exp_full[n - k:n].view(np.uint8)))
+                want = expect(op, np.arange(n - k, n, dtype=np.int64))
+                ok = bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
                 out.append({"op": op, "dtype": dtn, "bytes": nb, "us": round(us, 2),
                             "algbw_GiBps": round(nb / GiB / (us * 1e-6), 2), "checked": ok})
                 nb *= 4
@@ -112,6 +121,7 @@ def main() -> None:
     ap.add_argument("--no-combine", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--nelems", type=int, default=0, help="override: float32 elements per PE")
     ap.add_argument("--rccl", action="store_true",
                     help="N>1: also time RCCL all_reduce on the same payload (comparison only)")
@@ -259,6 +269,46 @@ def main() -> None:
         except Exception as ex:  # reported, never fatal for the main measurement
             extra["e2e_host"] = {"error": str(ex)}
 
+    if world > 1 and not args.no_probe:
+        # Measured link rates (report against the spec AND a measured L).  Plain
+        # pulls of a peer's source through the local combine kernel, no barriers inside:
+        #   pull1   — every rank copies S bytes from rank+1 (ring: each link busy in one direction)
+        #   pullall — every rank folds the sources of all p-1 peers (ingress (p-1)*S per GPU)
+        try:
+            S = min(B, 256 << 20)
+            ns = S // 4
+            peers = [(rank + d) % world for d in range(1, world)]
+            probe = {}
+            for name, srcs in (("pull1", [ish.ishmem_ptr(src, peers[0])]),
+                               ("pullall", [ish.ishmem_ptr(src, j) for j in peers])):
+                for _ in range(2):
+                    ish.combine("sum", "float", dst, srcs, ns, stream)
+                barrier()
+                k = 10
+                e0, e1 = hip.Event(), hip.Event()
+                e0.record(stream)
+                for _ in range(k):
+                    if ish.combine("sum", "float", dst, srcs, ns, stream) != 0:
+                        raise RuntimeError(ish.last_error())
+                e1.record(stream)
+                hip.stream_synchronize(stream)
+                ms = e0.elapsed_ms(e1) / k
+                import torch
+                tt = torch.tensor([ms], dtype=torch.float64)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                ms = float(tt[0])
+                gbs = len(srcs) * S / (ms * 1e-3) / 1e9
+                probe[name] = {"bytes_per_peer": S, "peers": len(srcs), "ms": round(ms, 4),
+                               "ingress_GBps": round(gbs, 1),
+                               "per_link_GBps": round(gbs / len(srcs), 1)}
+            barrier()
+            extra["xgmi_probe"] = probe
+            # Same accounting as roof["achieved"], against the measured all-peer ingress.
+            roof["peak_measured"] = probe["pullall"]["ingress_GBps"]
+            roof["frac_measured"] = roof["achieved"] / roof["peak_measured"]
+        except Exception as ex:
+            extra["xgmi_probe"] = {"error": str(ex)}
+
     if world > 1 and (args.rccl or os.environ.get("ISHMEM_BENCH_RCCL") == "1"):
         # Comparison only: RCCL (torch "nccl" backend) all_reduce of the same payload.
         try:
@@ -287,9 +337,9 @@ def main() -> None:
 
     if world > 1 and not args.no_sweep:
         # BASELINE configs[4] (min/max/prod x int32/float64 across the PEs), sizes 4 KiB ..
-        # 64 MiB per PE (the 4 GiB end of that sweep is left to tools/sweep.py).  Inputs
+        # the payload (1 GiB) per PE (the 4 GiB end of that sweep is left to tools/sweep.py).  Inputs
         # x_pe[i] = (i mod 1024) + pe; every result is checked against the canonical fold.
-        extra["config5_sweep"] = config5_sweep(ish, hip, src, dst, world, rank, dist, stream)
+        extra["config5_sweep"] = config5_sweep(ish, hip, src, dst, B, world, rank, dist, stream)
 
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:

@@ -45,9 +45,10 @@ struct ReduceArgs {
 
 // Small-message ("LL") path: 8-byte granules {4 data bytes | 32-bit epoch} pushed into every
 // peer's fine-grained receive ring; [parity 2][sender kMaxPes][kLLGranules] u64 per team.
-constexpr size_t kLLMaxBytes = 16384;                 // payload bytes per PE handled by LL
+constexpr size_t kLLMaxBytes = 65536;                 // LL ring capacity: payload bytes per PE
+constexpr size_t kLLDefaultBytes = 65536;             // default LL threshold (ISHMEM_LL_MAX_BYTES)
 constexpr size_t kLLGranules = kLLMaxBytes / 4;       // 4 payload bytes per granule
-constexpr size_t kLLTeamBytes = (size_t) 2 * kMaxPes * kLLGranules * 8;  // 1 MiB
+constexpr size_t kLLTeamBytes = (size_t) 2 * kMaxPes * kLLGranules * 8;  // 4 MiB
 struct LLArgs {
     const char *src;
     char *dst;

@@ -120,7 +120,7 @@ struct State {
 
     Team teams[kMaxTeams];
     int max_blocks = kMaxBlocks;
-    long long ll_max_bytes = (long long) kLLMaxBytes;
+    long long ll_max_bytes = (long long) kLLDefaultBytes;
     long long timeout_ms = 60000;
     int debug = 0;
     int error_count = 0;
@@ -658,7 +658,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, env_ll("ISHMEM_MAX_BLOCKS", kMaxBlocks)));
     s.timeout_ms = std::max<long long>(1, env_ll("ISHMEM_TIMEOUT_MS", 60000));
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
-                                         std::max<long long>(0, env_ll("ISHMEM_LL_MAX_BYTES", (long long) kLLMaxBytes)));
+                                         std::max<long long>(0, env_ll("ISHMEM_LL_MAX_BYTES", (long long) kLLDefaultBytes)));
     s.debug = (int) env_ll("ISHMEM_DEBUG", 0);
 
     int ndev = 0;

@@ -42,6 +42,11 @@ for s in $STEPS; do
     sweep1) run sweep1 300 python tools/sweep.py --max-mib 1024 ;;
     sweep2) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-256} run sweep2 600 python -m torch.distributed.run \
                 --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 tools/sweep.py --max-mib 256 ;;
+    llcmp)  for np_ in 2 4; do for ll in 0 65536; do
+              ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-128} ISHMEM_LL_MAX_BYTES=$ll run llcmp_p${np_}_ll${ll} 300 \
+                python -m torch.distributed.run --nnodes=1 --nproc-per-node $np_ --master-addr 127.0.0.1 \
+                --master-port 2952$np_ tools/sweep.py --max-mib 1 --min-bytes 2048 --factor 2 --iters 50
+            done; done ;;
     prof)   cd /tmp && export TMPDIR=/tmp
             run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                 python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline

@@ -43,15 +43,15 @@ def run_pes(npes: int, scenarios: list[str], timeout: float = 240.0, env: dict |
 @pytest.mark.parametrize("npes", [2, 4])
 @pytest.mark.parametrize("ll", ["on", "off"])
 def test_all_ops_types_vs_oracle_and_mpich_golden(npes, ll):
-    # ll=on: payloads <= 16 KiB take the one-hop granule path; ll=off forces reduce-scatter +
+    # ll=on: payloads <= 64 KiB take the one-hop granule path; ll=off forces reduce-scatter +
     # all-gather for the same inputs.
-    run_pes(npes, ["golden"], env={"ISHMEM_LL_MAX_BYTES": 16384 if ll == "on" else 0})
+    run_pes(npes, ["golden"], env={"ISHMEM_LL_MAX_BYTES": 65536 if ll == "on" else 0})
 
 
 @pytest.mark.parametrize("npes", [2, 3])
 @pytest.mark.parametrize("ll", ["on", "off"])
 def test_inplace_offsets_edges(npes, ll):
-    run_pes(npes, ["inplace", "offsets", "edge"], env={"ISHMEM_LL_MAX_BYTES": 16384 if ll == "on" else 0})
+    run_pes(npes, ["inplace", "offsets", "edge"], env={"ISHMEM_LL_MAX_BYTES": 65536 if ll == "on" else 0})
 
 
 def test_stream_staged_team():

@@ -21,6 +21,8 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-mib", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--min-bytes", type=int, default=4)
+    ap.add_argument("--factor", type=int, default=4)
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -44,9 +46,10 @@ def main() -> None:
     hip.upload(src, (np.arange(nmax, dtype=np.int64) % 1024).astype(np.float32) + np.float32(rank))
     st = hip.stream_create()
     if rank == 0:
-        print(f"# pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'}")
+        print(f"# pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
+              f"ll_max_bytes={ish.get_param('ll_max_bytes')}")
         print("bytes,us_per_call,algbw_GiBps,ok")
-    n = 1
+    n = max(1, args.min_bytes // 4)
     while n <= nmax:
         for _ in range(3):
             ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, st)
@@ -72,7 +75,7 @@ def main() -> None:
         ok = bool(np.array_equal(got, exp))
         if rank == 0:
             print(f"{n * 4},{us:.2f},{n * 4 / 2**30 / (us * 1e-6):.2f},{int(ok)}", flush=True)
-        n *= 4
+        n *= args.factor
     ish.ishmem_finalize()
 
 
