@@ -274,21 +274,23 @@ def main() -> None:
         # pulls of a peer's source through the local combine kernel, no barriers inside:
         #   pull1   — every rank copies S bytes from rank+1 (ring: each link busy in one direction)
         #   pullall — every rank folds the sources of all p-1 peers (ingress (p-1)*S per GPU)
+        #   push1   — every rank writes S bytes into rank+1's dest (remote stores)
         try:
             S = min(B, 256 << 20)
             ns = S // 4
             peers = [(rank + d) % world for d in range(1, world)]
             probe = {}
-            for name, srcs in (("pull1", [ish.ishmem_ptr(src, peers[0])]),
-                               ("pullall", [ish.ishmem_ptr(src, j) for j in peers])):
+            for name, srcs, out in (("pull1", [ish.ishmem_ptr(src, peers[0])], dst),
+                                    ("pullall", [ish.ishmem_ptr(src, j) for j in peers], dst),
+                                    ("push1", [src], ish.ishmem_ptr(dst, peers[0]))):
                 for _ in range(2):
-                    ish.combine("sum", "float", dst, srcs, ns, stream)
+                    ish.combine("sum", "float", out, srcs, ns, stream)
                 barrier()
                 k = 10
                 e0, e1 = hip.Event(), hip.Event()
                 e0.record(stream)
                 for _ in range(k):
-                    if ish.combine("sum", "float", dst, srcs, ns, stream) != 0:
+                    if ish.combine("sum", "float", out, srcs, ns, stream) != 0:
                         raise RuntimeError(ish.last_error())
                 e1.record(stream)
                 hip.stream_synchronize(stream)

@@ -173,7 +173,10 @@ void *ishmemi_c_device_ctx(void);
 
 /* ---- diagnostics / parameters ----------------------------------------------------------------
  * ishmemi_c_set_param names: "max_blocks" (workgroups per collective launch, <= 1024),
- * "timeout_ms" (bound on every device-side spin), "debug". */
+ * "ll_max_bytes" (one-hop granule path threshold, <= 65536), "timeout_ms" (bound on every
+ * device-side spin), "debug".  "max_blocks" and "ll_max_bytes" shape every multi-PE launch: init
+ * agrees on them (minimum over the PEs); a later set_param must be made with the same value on
+ * every PE.  ishmemi_c_get_param also reports "staging_bytes" and "flags_fine_grained". */
 const char *ishmemi_c_last_error(void);
 int ishmemi_c_set_param(const char *name, long long value);
 long long ishmemi_c_get_param(const char *name);

@@ -13,6 +13,12 @@
  *       int rc = ishmemx_float_sum_reduce_work_group(ctx, dst, src, n);
  *   }
  *
+ * The trailing group argument selects who calls: `ishmemx_dev::work_group` (default, every
+ * thread of the work-group) or `ishmemx_dev::wavefront` (one full 64-lane wavefront — the
+ * reference's sycl::sub_group overload).  The device-side blocking call of the reference
+ * (`ishmem_<TYPENAME>_<op>_reduce` from inside a kernel, e.g. in a single_task) is
+ * `ishmem_<TYPENAME>_<op>_reduce(ctx, [team,] dest, source, nreduce)` called by ONE work-item.
+ *
  * Algorithm: the same direct reduce-scatter + all-gather as the host-launched kernel, executed by
  * the calling work-group (member c folds chunk c of every member's source in canonical team order
  * with system-coherent loads, stores it write-through, team barrier, then pulls the other chunks).
@@ -78,15 +84,48 @@ __device__ __forceinline__ char *peer_addr(const ishmemi_c_device_ctx_t *c, cons
     return c->peer_heap[pe] + ((const char *) p - c->heap_base);
 }
 
-// Team barrier among the calling work-groups (one per member): thread 0 stores the epoch into
-// its slot of every peer's row and polls its own row; bounded by the library timeout.
-__device__ inline bool wg_barrier(const ishmemi_c_device_ctx_t *c, int team, int phase,
-                                  uint32_t epoch, bool release)
+// Execution groups that can call a device collective (the reference's `const Group &grp`:
+// sycl::group<1..3> and sycl::sub_group, plus the single work-item of a device-side blocking
+// call).  Every member of the group calls with identical arguments.
+struct work_group_t {  // every thread of the work-group
+    __device__ static int rank() { return threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z); }
+    __device__ static int size() { return blockDim.x * blockDim.y * blockDim.z; }
+    __device__ static void sync() { __syncthreads(); }
+    __device__ static uint32_t bcast(uint32_t v)
+    {
+        __shared__ uint32_t s_v;
+        __syncthreads();
+        if (rank() == 0) s_v = v;
+        __syncthreads();
+        return s_v;
+    }
+};
+struct wavefront_t {  // one full 64-lane wavefront (sub_group analogue)
+    __device__ static int rank() { return (int) __lane_id(); }
+    __device__ static int size() { return warpSize; }
+    __device__ static void sync() { __builtin_amdgcn_wave_barrier(); }
+    __device__ static uint32_t bcast(uint32_t v) { return (uint32_t) __shfl((int) v, 0); }
+};
+struct thread_t {  // one work-item (device-side ishmem_<TN>_<op>_reduce)
+    __device__ static int rank() { return 0; }
+    __device__ static int size() { return 1; }
+    __device__ static void sync() {}
+    __device__ static uint32_t bcast(uint32_t v) { return v; }
+};
+inline constexpr work_group_t work_group{};
+inline constexpr wavefront_t wavefront{};
+inline constexpr thread_t thread{};
+
+// Team barrier among the calling groups (one per member): the group's leader stores the epoch
+// into its slot of every peer's row and polls its own row; bounded by the library timeout.
+template <typename G>
+__device__ inline bool group_barrier(const ishmemi_c_device_ctx_t *c, int team, int phase,
+                                     uint32_t epoch, bool release)
 {
-    __shared__ int s_ok;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x + threadIdx.y + threadIdx.z == 0) {
+    G::sync();
+    uint32_t ok = 1;
+    if (G::rank() == 0) {
         const int size = c->team_size[team], me = c->team_my_idx[team];
         const size_t row = ((size_t) team * ISHMEMI_C_DEV_PHASES + phase) * ISHMEMI_C_MAX_PES;
         if (release) {
@@ -99,14 +138,13 @@ __device__ inline bool wg_barrier(const ishmemi_c_device_ctx_t *c, int team, int
             __hip_atomic_store(c->peer_dflags[gpe] + row + me, epoch, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        bool ok = true;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (int j = 0; j < size && ok; ++j) {
             if (j == me) continue;
             while ((int32_t) (__hip_atomic_load(c->my_dflags + row + j, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > c->timeout_ticks) {
-                    ok = false;
+                    ok = 0;
                     __hip_atomic_fetch_or(c->err, 1u << phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
@@ -114,33 +152,29 @@ __device__ inline bool wg_barrier(const ishmemi_c_device_ctx_t *c, int team, int
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        s_ok = ok;
     }
-    __syncthreads();
-    return s_ok != 0;
+    return G::bcast(ok) != 0;
 }
 
-template <typename T, int OP>
-__device__ int reduce_work_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, const T *source,
-                                 size_t nreduce)
+template <typename G, typename T, int OP>
+__device__ int reduce_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, const T *source,
+                            size_t nreduce)
 {
-    __shared__ uint32_t s_epoch;
-    const int tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
-    const int nthr = blockDim.x * blockDim.y * blockDim.z;
+    const int tid = G::rank(), nthr = G::size();
     const int size = c->team_size[team], me = c->team_my_idx[team];
     if (size <= 0 || me < 0) return 1;
+    uint32_t epoch = 0;
     if (tid == 0)
-        s_epoch = __hip_atomic_fetch_add(c->epochs + team, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    __syncthreads();
-    const uint32_t epoch = s_epoch;
+        epoch = __hip_atomic_fetch_add(c->epochs + team, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    epoch = G::bcast(epoch);
     if (size == 1) {  // one PE: dest = source (reduce_impl.h:288-289)
         if (dest != source)
             for (size_t i = tid; i < nreduce; i += nthr) dest[i] = source[i];
-        __syncthreads();
+        G::sync();
         return 0;
     }
-    // Start: every member's source is complete (this work-group's own writes released).
-    if (!wg_barrier(c, team, 0, epoch, true)) return 1;
+    // Start: every member's source is complete (this group's own writes released).
+    if (!group_barrier<G>(c, team, 0, epoch, true)) return 1;
     const size_t per = ((nreduce + size - 1) / size + 63) & ~(size_t) 63;
     const size_t cs = (size_t) me * per < nreduce ? (size_t) me * per : nreduce;
     const size_t ce = cs + per < nreduce ? cs + per : nreduce;
@@ -154,7 +188,7 @@ __device__ int reduce_work_group(const ishmemi_c_device_ctx_t *c, int team, T *d
         }
         sys_store(dest + i, acc);  // write-through: peers pull it after the next barrier
     }
-    if (!wg_barrier(c, team, 1, epoch, true)) return 1;
+    if (!group_barrier<G>(c, team, 1, epoch, true)) return 1;
     for (int k = 1; k < size; ++k) {
         const int j = (me + k) % size;
         const int gpe = start + j * stride;
@@ -163,7 +197,14 @@ __device__ int reduce_work_group(const ishmemi_c_device_ctx_t *c, int team, T *d
         for (size_t i = js + tid; i < je; i += nthr) dest[i] = sys_load((const T *) peer_addr(c, dest + i, gpe));
     }
     // End: no member returns while a peer may still read its dest.
-    return wg_barrier(c, team, 2, epoch, false) ? 0 : 1;
+    return group_barrier<G>(c, team, 2, epoch, false) ? 0 : 1;
+}
+
+template <typename T, int OP>
+__device__ int reduce_work_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, const T *source,
+                                 size_t nreduce)
+{
+    return reduce_group<work_group_t, T, OP>(c, team, dest, source, nreduce);
 }
 
 template <typename T>
@@ -175,18 +216,33 @@ constexpr bool is_canon()
 }  // namespace ishmemx_dev
 
 #define ISHMEMX_DEV_GENERIC(OPNAME, OPC)                                                           \
-    template <typename T>                                                                          \
+    template <typename T, typename G = ishmemx_dev::work_group_t>                                  \
     __device__ inline int ishmemx_##OPNAME##_reduce_work_group(                                    \
-        const ishmemi_c_device_ctx_t *ctx, T *dest, const T *source, size_t nreduce)               \
+        const ishmemi_c_device_ctx_t *ctx, T *dest, const T *source, size_t nreduce, G = G())      \
     {                                                                                              \
-        return ishmemx_dev::reduce_work_group<T, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,     \
-                                                      nreduce);                                    \
+        return ishmemx_dev::reduce_group<G, T, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,       \
+                                                    nreduce);                                      \
+    }                                                                                              \
+    template <typename T, typename G = ishmemx_dev::work_group_t>                                  \
+    __device__ inline int ishmemx_##OPNAME##_reduce_work_group(                                    \
+        const ishmemi_c_device_ctx_t *ctx, int team, T *dest, const T *source, size_t nreduce,     \
+        G = G())                                                                                   \
+    {                                                                                              \
+        return ishmemx_dev::reduce_group<G, T, OPC>(ctx, team, dest, source, nreduce);             \
     }                                                                                              \
     template <typename T>                                                                          \
-    __device__ inline int ishmemx_##OPNAME##_reduce_work_group(                                    \
-        const ishmemi_c_device_ctx_t *ctx, int team, T *dest, const T *source, size_t nreduce)     \
+    __device__ inline int ishmem_##OPNAME##_reduce(const ishmemi_c_device_ctx_t *ctx, T *dest,     \
+                                                   const T *source, size_t nreduce)                \
     {                                                                                              \
-        return ishmemx_dev::reduce_work_group<T, OPC>(ctx, team, dest, source, nreduce);           \
+        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, T, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, \
+                                                                        dest, source, nreduce);    \
+    }                                                                                              \
+    template <typename T>                                                                          \
+    __device__ inline int ishmem_##OPNAME##_reduce(const ishmemi_c_device_ctx_t *ctx, int team,    \
+                                                   T *dest, const T *source, size_t nreduce)       \
+    {                                                                                              \
+        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, T, OPC>(ctx, team, dest, source,   \
+                                                                        nreduce);                  \
     }
 
 ISHMEMX_DEV_GENERIC(and, ISHMEMI_OP_AND)
@@ -198,17 +254,33 @@ ISHMEMX_DEV_GENERIC(sum, ISHMEMI_OP_SUM)
 ISHMEMX_DEV_GENERIC(prod, ISHMEMI_OP_PROD)
 
 #define ISHMEMX_DEV_TYPED(TYPENAME, TYPE, OPNAME, OPC)                                              \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
     __device__ inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_work_group(                       \
+        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nreduce,         \
+        G = G())                                                                                   \
+    {                                                                                              \
+        return ishmemx_dev::reduce_group<G, TYPE, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,    \
+                                                       nreduce);                                   \
+    }                                                                                              \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
+    __device__ inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_work_group(                       \
+        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source,               \
+        size_t nreduce, G = G())                                                                   \
+    {                                                                                              \
+        return ishmemx_dev::reduce_group<G, TYPE, OPC>(ctx, team, dest, source, nreduce);          \
+    }                                                                                              \
+    __device__ inline int ishmem_##TYPENAME##_##OPNAME##_reduce(                                   \
         const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nreduce)         \
     {                                                                                              \
-        return ishmemx_dev::reduce_work_group<TYPE, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,  \
-                                                         nreduce);                                 \
+        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, TYPE, OPC>(                        \
+            ctx, ISHMEMI_C_TEAM_WORLD, dest, source, nreduce);                                     \
     }                                                                                              \
-    __device__ inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_work_group(                       \
+    __device__ inline int ishmem_##TYPENAME##_##OPNAME##_reduce(                                   \
         const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source,               \
         size_t nreduce)                                                                            \
     {                                                                                              \
-        return ishmemx_dev::reduce_work_group<TYPE, OPC>(ctx, team, dest, source, nreduce);        \
+        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, TYPE, OPC>(ctx, team, dest,        \
+                                                                           source, nreduce);       \
     }
 
 /* Same TYPENAME x op matrix as the host API (src/collectives/reduce.cpp:95-417). */

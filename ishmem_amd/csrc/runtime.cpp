@@ -88,6 +88,10 @@ struct Team {
 struct PeRecord {
     int32_t pe, pid, device, flags_fine_grained;
     uint64_t heap_size;
+    // Launch-shape parameters: the multi-PE kernels pair workgroup b with workgroup b of every
+    // peer and choose the LL path per call, so every PE must use the same values.
+    int64_t max_blocks, ll_max_bytes;
+    uint64_t staging_bytes;
     hipIpcMemHandle_t heap_handle;
     hipIpcMemHandle_t flags_handle;
 };
@@ -660,6 +664,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
                                          std::max<long long>(0, env_ll("ISHMEM_LL_MAX_BYTES", (long long) kLLDefaultBytes)));
     s.debug = (int) env_ll("ISHMEM_DEBUG", 0);
+    s.staging_bytes = (parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20) + kHeapAlign - 1) &
+                      ~(size_t) (kHeapAlign - 1);
 
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
@@ -710,6 +716,9 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.device = s.device;
         mine.flags_fine_grained = s.flags_fine_grained ? 1 : 0;
         mine.heap_size = s.heap_size;
+        mine.max_blocks = s.max_blocks;
+        mine.ll_max_bytes = s.ll_max_bytes;
+        mine.staging_bytes = s.staging_bytes;
         HIP_TRY(hipIpcGetMemHandle(&mine.heap_handle, s.heap));
         if (hipIpcGetMemHandle(&mine.flags_handle, s.flags) != hipSuccess) {
             // Uncached allocations that cannot be exported: fall back to coarse-grained flags
@@ -726,6 +735,13 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         }
         PeRecord all[kMaxPes];
         if (s.boot.allgather(&mine, all, sizeof(PeRecord), err)) return fail(err);
+        // Agree on the launch-shape parameters (the minimum over the PEs), so a per-process
+        // environment difference cannot pair mismatched grids or split LL from RS/AG.
+        for (int j = 0; j < npes; ++j) {
+            s.max_blocks = (int) std::min<int64_t>(s.max_blocks, all[j].max_blocks);
+            s.ll_max_bytes = std::min<long long>(s.ll_max_bytes, all[j].ll_max_bytes);
+            s.staging_bytes = std::min<size_t>(s.staging_bytes, all[j].staging_bytes);
+        }
         for (int j = 0; j < npes; ++j) {
             if (j == pe) continue;
             if (all[j].heap_size != s.heap_size)
@@ -762,7 +778,6 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         t.my_idx = pe;
     }
     // Symmetric staging region (first allocation on every PE, hence the same offset).
-    s.staging_bytes = parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20);
     s.staging = (char *) heap_alloc(s, s.staging_bytes, kHeapAlign);
     if (!s.staging) return 1;
     s.team_scratch = (char *) heap_alloc(s, kHeapAlign, kHeapAlign);

@@ -3,6 +3,7 @@
 // work-group per PE, checked against the closed form ((1 << npes) - 1) << 40 + idx * npes) and
 // of its reduce_*.cpp pattern tests (sources = reference source patterns, checked against the
 // reference check patterns restated in oracle/oracle.c, linked here as the CHECKER).
+// Also: a wavefront (sub_group) caller and a single work-item device-side ishmem_int_sum_reduce.
 // Launch: ISHMEM_PE=<pe> ISHMEM_NPES=<n> ISHMEM_DEVICE=0 ISHMEM_BOOTSTRAP_KEY=<k> ./device_wg
 #include <hip/hip_runtime.h>
 
@@ -41,6 +42,43 @@ __global__ void pattern_kernel(const ishmemi_c_device_ctx_t *ctx, int team, T *d
     else if constexpr (OPC == ISHMEMI_OP_OR) r = ishmemx_or_reduce_work_group(ctx, team, dest, source, n);
     else r = ishmemx_xor_reduce_work_group(ctx, team, dest, source, n);
     if (threadIdx.x == 0) *rc = r;
+}
+
+// sub_group analogue: only the second wavefront of the work-group takes part.
+__global__ void wave_kernel(const ishmemi_c_device_ctx_t *ctx, float *dest, const float *source, size_t n,
+                            int *rc)
+{
+    if (threadIdx.x / warpSize != 1) return;
+    const int r = ishmemx_float_sum_reduce_work_group(ctx, dest, source, n, ishmemx_dev::wavefront);
+    if (__lane_id() == 0) *rc = r;
+}
+
+// Device-side blocking call by one work-item (the reference's single_task shape).
+__global__ void single_kernel(const ishmemi_c_device_ctx_t *ctx, int *dest, const int *source, size_t n,
+                              int *rc)
+{
+    *rc = ishmem_int_sum_reduce(ctx, ISHMEM_TEAM_WORLD, dest, source, n);
+}
+
+template <typename K, typename T, int OPC, int ODT>
+static void group_case(const char *what, K kernel, int block, const ishmemi_c_device_ctx_t *ctx, size_t n,
+                       char *sb, char *db, int *rc)
+{
+    const int pe = ishmem_my_pe(), npes = ishmem_n_pes();
+    std::vector<T> src(n), chk(n), got(n);
+    oracle_pattern_source(PAT_ARITH, ODT, pe, n, src.data());
+    oracle_pattern_check(PAT_ARITH, OPC, ODT, npes, n, chk.data());
+    (void) hipMemcpy(sb, src.data(), n * sizeof(T), hipMemcpyHostToDevice);
+    (void) hipMemset(db, 0, n * sizeof(T));
+    (void) hipMemset(rc, 0xff, sizeof(int));
+    hipLaunchKernelGGL(kernel, dim3(1), dim3(block), 0, 0, ctx, (T *) db, (const T *) sb, n, rc);
+    (void) hipDeviceSynchronize();
+    int r = -1;
+    (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);
+    (void) hipMemcpy(got.data(), db, n * sizeof(T), hipMemcpyDeviceToHost);
+    if (r != 0 || memcmp(got.data(), chk.data(), n * sizeof(T)) != 0) {
+        if (++errors <= 16) printf("[%d] FAIL %s n %zu rc %d\n", pe, what, n, r);
+    }
 }
 
 template <typename T, int OPC, int ODT>
@@ -105,6 +143,12 @@ int main()
         pattern_case<uint64_t, OR_XOR, OD_UINT64>(ctx, n, 512, sb, db, rc);
         pattern_case<uint8_t, OR_AND, OD_UINT8>(ctx, n, 256, sb, db, rc);
         pattern_case<uint32_t, OR_OR, OD_UINT32>(ctx, n, 256, sb, db, rc);
+    }
+    for (size_t n : {1, 63, 64, 1000, 20000}) {
+        group_case<decltype(&wave_kernel), float, OR_SUM, OD_FLOAT>("wavefront float sum", wave_kernel, 256, ctx,
+                                                                    n, sb, db, rc);
+        group_case<decltype(&single_kernel), int, OR_SUM, OD_INT32>("single-thread int sum", single_kernel, 1,
+                                                                    ctx, n, sb, db, rc);
     }
     ishmem_free(rc);
     ishmem_free(db);

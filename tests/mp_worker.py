@@ -24,8 +24,8 @@ def _bits_equal(a, b):
 def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None = None) -> None:
     fails: list[str] = []
     try:
-        for k, v in (env or {}).items():
-            os.environ[k] = str(v)
+        for k, v in (env or {}).items():  # a list gives each PE its own value
+            os.environ[k] = str(v[pe] if isinstance(v, list) else v)
         import oracle
         import ishmem_amd as ish
         from ishmem_amd import hip

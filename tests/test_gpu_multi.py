@@ -70,3 +70,12 @@ def test_huge_2p5GiB_per_pe_head_tail_and_2GiB_boundary():
 def test_fcollect_collect_scan_vs_tester_patterns_and_oracle(npes):
     # Small staging region so the scan's segment loop runs several times.
     run_pes(npes, ["collect", "scan"], env={"ISHMEM_STAGING_SIZE": "4M"}, timeout=300)
+
+
+def test_launch_parameters_agreed_at_init():
+    # Per-PE environments that disagree on the grid cap, the LL threshold and the staging size:
+    # init takes the minimum, so the collectives still pair up (a mismatch would otherwise split
+    # LL from RS/AG or pair different grids and time out).
+    run_pes(3, ["inplace", "offsets", "staged"],
+            env={"ISHMEM_MAX_BLOCKS": [32, 8, 64], "ISHMEM_LL_MAX_BYTES": [65536, 0, 4096],
+                 "ISHMEM_STAGING_SIZE": ["4M", "8M", "2M"]})
