@@ -120,6 +120,11 @@ struct State {
     char *staging = nullptr;  // symmetric staging region for non-heap / host buffers
     size_t staging_bytes = 0;
     hipStream_t copy_in = nullptr, copy_out = nullptr;  // staging pipeline streams
+    // Stream of the previous collective: a collective enqueued on another stream first waits
+    // for it, so epochs, flag rows and the staging region are used in call order.
+    hipStream_t last_stream = nullptr;
+    bool last_stream_set = false;
+    hipEvent_t order_ev = nullptr;
     hipEvent_t ev_in[2] = {}, ev_red[2] = {}, ev_out[2] = {};
 
     Team teams[kMaxTeams];
@@ -329,9 +334,37 @@ bool ll_eligible(const State &s, const Team &t, const void *dst, const void *src
            bytes <= kLLMaxBytes && (((uintptr_t) dst | (uintptr_t) src) & 7) == 0;
 }
 
+// Collectives of one PE run in the order they were called, whatever streams they were enqueued
+// on (the flag protocol pairs the k-th collective of a team on every PE; the staging region is
+// shared).  Same stream as last time: nothing to do.
+// The switch is handled when it happens: an event recorded on the previous stream, waited on by
+// the new one (no per-call event: a recorded event costs microseconds of device time).  If the
+// previous stream has been destroyed since, the record fails and the device is drained instead.
+int order_stream(State &s, hipStream_t st)
+{
+    if (s.last_stream_set && s.last_stream != st) {
+        if (!s.order_ev) HIP_TRY(hipEventCreateWithFlags(&s.order_ev, hipEventDisableTiming));
+        if (hipEventRecord(s.order_ev, s.last_stream) == hipSuccess) {
+            HIP_TRY(hipStreamWaitEvent(st, s.order_ev, 0));
+        } else {
+            (void) hipGetLastError();
+            HIP_TRY(hipDeviceSynchronize());
+        }
+    }
+    return 0;
+}
+
+int mark_stream(State &s, hipStream_t st)
+{
+    s.last_stream = st;
+    s.last_stream_set = true;
+    return 0;
+}
+
 int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, size_t bytes, int *ret,
               hipStream_t st)
 {
+    if (order_stream(s, st)) return 1;
     Team &t = s.teams[team];
     LLArgs a;
     memset(&a, 0, sizeof(a));
@@ -359,6 +392,7 @@ int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, si
 int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, size_t n, int *ret,
                 hipStream_t st)
 {
+    if (order_stream(s, st)) return 1;
     Team &t = s.teams[team];
     const size_t es = dtype_size(dt);
     ReduceArgs a;
@@ -395,6 +429,7 @@ int reduce_staged(State &s, int team, int op, int dt, void *dst, const void *src
     const size_t slot_bytes = (s.staging_bytes / 2) & ~(kHeapAlign - 1);
     const size_t chunk = (slot_bytes / es) & ~size_t(63);
     if (chunk == 0) return fail("reduce: staging region too small");
+    if (order_stream(s, st)) return 1;
     if (!s.copy_in) {
         HIP_TRY(hipStreamCreateWithFlags(&s.copy_in, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&s.copy_out, hipStreamNonBlocking));
@@ -457,6 +492,7 @@ int collect_launch(State &s, int team, void *dst, const void *src, const uint64_
                    hipStream_t st)
 {
     Team &t = s.teams[team];
+    if (order_stream(s, st)) return 1;
     CollectArgs a;
     memset(&a, 0, sizeof(a));
     std::string why;
@@ -499,6 +535,7 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
         for (int j = 0; j < t.size; ++j) nb[j] = nbytes;
         if (collect_launch(s, team, dst, src, nb, ret, st)) return 1;
     }
+    if (mark_stream(s, st)) return 1;
     if (blocking) {
         HIP_TRY(hipStreamSynchronize(st));
         if (check_team_errors(s, team)) return 1;
@@ -530,6 +567,7 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
         const uint64_t ipc_max = ((s.staging_bytes / es) / (uint64_t) t.size) & ~uint64_t(63);
         const uint64_t seg = ipc_max * (uint64_t) t.size;
         if (ipc_max == 0) return fail("scan: staging region too small for this team");
+        if (order_stream(s, st)) return 1;
         for (uint64_t off = 0; off < n; off += seg) {
             const uint64_t m = std::min<uint64_t>(seg, n - off);
             ScanArgs a;
@@ -552,6 +590,7 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
             HIP_TRY(launch_scan(dt, a, grid, st));
         }
     }
+    if (mark_stream(s, st)) return 1;
     if (blocking) {
         HIP_TRY(hipStreamSynchronize(st));
         if (check_team_errors(s, team)) return 1;
@@ -563,6 +602,7 @@ int team_sync_locked(State &s, int team, hipStream_t st, int *ret)
 {
     Team &t = s.teams[team];
     if (t.size <= 1) return 0;
+    if (order_stream(s, st)) return 1;
     ReduceArgs a;
     std::string why;
     if (team_args(s, team, a, why)) return fail("team_sync: " + why);
@@ -610,6 +650,7 @@ int reduce_impl(int team, int op, int dt, void *dst, const void *src, size_t n, 
     } else {
         if (reduce_staged(s, team, op, dt, dst, src, n, ret, st)) return 1;
     }
+    if (mark_stream(s, st)) return 1;
     if (blocking) {
         HIP_TRY(hipStreamSynchronize(st));
         if (check_team_errors(s, team)) return 1;
@@ -862,6 +903,10 @@ int ishmemi_c_finalize(void)
     (void) hipHostFree(s.err_host);
     (void) hipFree(s.dctx);
     (void) hipFree(s.dev_epochs);
+    if (s.order_ev) (void) hipEventDestroy(s.order_ev);
+    s.order_ev = nullptr;
+    s.last_stream = nullptr;
+    s.last_stream_set = false;
     s.dctx = nullptr;
     s.dev_epochs = nullptr;
     s.heap = nullptr;
@@ -1084,7 +1129,7 @@ int ishmemi_c_team_sync(int team)
     if (!s.initialized) return fail("team_sync: not initialized");
     if (team < 0 || team >= kMaxTeams || !s.teams[team].valid) return fail("team_sync: invalid team");
     if (s.teams[team].my_idx < 0) return fail("team_sync: caller not in team");
-    if (team_sync_locked(s, team, 0, nullptr)) return 1;
+    if (team_sync_locked(s, team, 0, nullptr) || mark_stream(s, 0)) return 1;
     HIP_TRY(hipStreamSynchronize(0));
     return check_team_errors(s, team);
 }
@@ -1161,7 +1206,7 @@ int ishmemi_c_collect(int team, void *dest, const void *source, size_t nbytes)
         return fail("collect: count copy failed");
     std::lock_guard<std::mutex> lk(s.mu);
     if (!in_heap(s, dest)) return fail("collect: dest must be symmetric-heap memory");
-    if (collect_launch(s, team, dest, source, counts, nullptr, 0)) return 1;
+    if (collect_launch(s, team, dest, source, counts, nullptr, 0) || mark_stream(s, 0)) return 1;
     HIP_TRY(hipStreamSynchronize(0));
     return check_team_errors(s, team);
 }

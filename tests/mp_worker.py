@@ -155,6 +155,37 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             for p in (ret, d, s):
                 ish.ishmem_free(p)
 
+        if "streams" in scenarios:
+            # Back-to-back collectives on different streams with no host synchronisation between
+            # them (each must follow the previous one: same epochs / flag rows / staging on every
+            # PE), the last stream destroyed before a blocking call.
+            n = 70_000
+            ins = [[oracle.fill_random(DT["int32"], 300 + 10 * r + j, n) for j in range(npes)] for r in range(4)]
+            s_b = [heap(n, DT["int32"]) for _ in range(4)]
+            d_b = [heap(n, DT["int32"]) for _ in range(4)]
+            for r in range(4):
+                hip.upload(s_b[r], ins[r][pe])
+            sts = [hip.stream_create() for _ in range(3)]
+            host_out = np.zeros(n, np.int32)
+            host_in = np.ascontiguousarray(ins[3][pe])
+            calls = [ish.ishmemx_int32_sum_reduce_on_stream(d_b[0], s_b[0], n, 0, sts[0]),
+                     ish.ishmemx_int32_max_reduce_on_stream(d_b[1], s_b[1], n, 0, sts[1]),
+                     ish.ishmemx_int32_sum_reduce_on_stream(d_b[2], s_b[2], 1000, 0, sts[2]),  # LL
+                     ish.ishmemx_int32_xor_reduce_on_stream(host_out.ctypes.data, host_in.ctypes.data, n, 0, sts[0])]
+            hip.stream_destroy(sts[2])
+            if any(calls) or ish.ishmem_int32_min_reduce(d_b[3], s_b[3], n):
+                fails.append(f"pe{pe} streams rc={calls} {ish.last_error()}")
+            hip.synchronize()
+            check("streams sum", OPS["sum"], DT["int32"], ins[0], hip.download(d_b[0], n, np.int32))
+            check("streams max", OPS["max"], DT["int32"], ins[1], hip.download(d_b[1], n, np.int32))
+            check("streams ll", OPS["sum"], DT["int32"], [x[:1000] for x in ins[2]], hip.download(d_b[2], 1000, np.int32))
+            check("streams host", OPS["xor"], DT["int32"], ins[3], host_out)
+            check("streams min", OPS["min"], DT["int32"], ins[3], hip.download(d_b[3], n, np.int32))
+            for st_ in sts[:2]:
+                hip.stream_destroy(st_)
+            for b in s_b + d_b:
+                ish.ishmem_free(b)
+
         if "staged" in scenarios:
             # Host memory and device memory outside the heap go through the staging region.
             n = 300_000

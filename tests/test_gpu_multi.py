@@ -55,7 +55,7 @@ def test_inplace_offsets_edges(npes, ll):
 
 
 def test_stream_staged_team():
-    run_pes(4, ["stream", "staged", "team"])
+    run_pes(4, ["stream", "streams", "staged", "team"])
 
 
 def test_large_f32_sum_256MiB_per_pe():
