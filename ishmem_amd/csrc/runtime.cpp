@@ -290,7 +290,9 @@ int check_team_errors(State &s, int team)
     if (e) {
         __atomic_store_n(&s.err_host[team], 0u, __ATOMIC_RELEASE);
         s.error_count++;
-        return fail("device barrier timed out (phase mask 0x" + std::to_string(e) +
+        char mask[16];
+        snprintf(mask, sizeof(mask), "0x%x", e);
+        return fail(std::string("device barrier timed out (phase mask ") + mask +
                     "): a team member did not arrive within timeout_ms");
     }
     return 0;

@@ -47,6 +47,11 @@ for s in $STEPS; do
                 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np_ --master-addr 127.0.0.1 \
                 --master-port 2952$np_ tools/sweep.py --max-mib 1 --min-bytes 2048 --factor 2 --iters 50
             done; done ;;
+    coll)   for c in fcollect inscan; do
+              ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-256} run coll_${c}_p2 300 \
+                python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+                --master-port 29541 tools/sweep.py --coll $c --max-mib 256 --min-bytes 4096 --factor 4
+            done ;;
     prof)   cd /tmp && export TMPDIR=/tmp
             run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                 python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline

@@ -52,6 +52,27 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 elif not _bits_equal(golden, got):
                     fails.append(f"pe{pe} {tag}: differs from MPICH golden")
 
+        if "timeout" in scenarios:
+            # Failure detection: PE 0 enters collectives PE 1 never joins.  Every device-side
+            # spin is bounded, so the call returns nonzero with a diagnostic instead of hanging
+            # (LL granule path and three-barrier path).  The team's epochs now disagree, so the
+            # job ends here, as after any collective error.
+            ish.set_param("timeout_ms", 300)
+            s_b, d_b = heap(1 << 20, DT["float"]), heap(1 << 20, DT["float"])
+            if pe == 0:
+                for n in (100, 1 << 20):
+                    r = ish.ishmem_float_sum_reduce(d_b, s_b, n)
+                    msg = ish.last_error()
+                    if r == 0:
+                        fails.append(f"pe0 n={n}: expected a timeout error, got success")
+                    elif "timed out" not in msg:
+                        fails.append(f"pe0 n={n}: unexpected error text: {msg}")
+                if ish.lib().ishmemi_c_error_count() != 2:
+                    fails.append(f"pe0 error_count {ish.lib().ishmemi_c_error_count()} != 2")
+            ish.ishmem_finalize()
+            q.put((pe, fails))
+            return
+
         if "golden" in scenarios:
             z = np.load(GOLDEN / f"golden_np{npes}.npz") if (GOLDEN / f"golden_np{npes}.npz").exists() else None
             for op in range(7):

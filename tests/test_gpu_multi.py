@@ -79,3 +79,7 @@ def test_launch_parameters_agreed_at_init():
     run_pes(3, ["inplace", "offsets", "staged"],
             env={"ISHMEM_MAX_BLOCKS": [32, 8, 64], "ISHMEM_LL_MAX_BYTES": [65536, 0, 4096],
                  "ISHMEM_STAGING_SIZE": ["4M", "8M", "2M"]})
+
+
+def test_missing_member_times_out_with_error_instead_of_hanging():
+    run_pes(2, ["timeout"], timeout=120)

@@ -23,6 +23,7 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--min-bytes", type=int, default=4)
     ap.add_argument("--factor", type=int, default=4)
+    ap.add_argument("--coll", choices=["reduce", "fcollect", "inscan"], default="reduce")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -42,17 +43,32 @@ def main() -> None:
     ish.init(rank, world, dev, key)
     nmax = (args.max_mib << 20) // 4
     src = ish.ishmem_malloc(nmax * 4)
-    dst = ish.ishmem_malloc(nmax * 4)
+    dst = ish.ishmem_malloc(nmax * 4 * (world if args.coll == "fcollect" else 1))
     hip.upload(src, (np.arange(nmax, dtype=np.int64) % 1024).astype(np.float32) + np.float32(rank))
     st = hip.stream_create()
     if rank == 0:
-        print(f"# pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
+        print(f"# coll={args.coll} pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
               f"ll_max_bytes={ish.get_param('ll_max_bytes')}")
         print("bytes,us_per_call,algbw_GiBps,ok")
+    def call(n):
+        if args.coll == "fcollect":
+            return ish.fcollect_on_stream(dst, src, n * 4, 0, st)
+        if args.coll == "inscan":
+            return ish.lib().ishmemi_c_scan_on_stream(0, ish.DTYPES["float"], 1, dst, src, n, None, st)
+        return ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, st)
+
+    def expect(i, n):
+        base = (i % 1024).astype(np.float32)
+        if args.coll == "fcollect":  # the last k elements of the dest = PE world-1's tail
+            return base + np.float32(world - 1)
+        if args.coll == "inscan":
+            return base * (rank + 1) + np.float32(rank * (rank + 1) / 2)
+        return base * world + np.float32(world * (world - 1) / 2)
+
     n = max(1, args.min_bytes // 4)
     while n <= nmax:
         for _ in range(3):
-            ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, st)
+            call(n)
         hip.stream_synchronize(st)
         if dist is not None:
             dist.barrier()
@@ -60,7 +76,8 @@ def main() -> None:
         iters = args.iters if n < (1 << 24) else max(3, args.iters // 4)
         e0.record(st)
         for _ in range(iters):
-            ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, st)
+            if call(n):
+                raise RuntimeError(ish.last_error())
         e1.record(st)
         hip.stream_synchronize(st)
         us = e0.elapsed_ms(e1) * 1000.0 / iters
@@ -69,10 +86,9 @@ def main() -> None:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             us = float(t[0])
         k = min(n, 64)
-        got = hip.download(dst + (n - k) * 4, k, np.float32)
-        i = np.arange(n - k, n)
-        exp = (i % 1024).astype(np.float32) * world + np.float32(world * (world - 1) / 2)
-        ok = bool(np.array_equal(got, exp))
+        last = n * (world if args.coll == "fcollect" else 1)
+        got = hip.download(dst + (last - k) * 4, k, np.float32)
+        ok = bool(np.array_equal(got, expect(np.arange(n - k, n), n)))
         if rank == 0:
             print(f"{n * 4},{us:.2f},{n * 4 / 2**30 / (us * 1e-6):.2f},{int(ok)}", flush=True)
         n *= args.factor
