@@ -96,7 +96,7 @@ struct ScanArgs {
     int p, me;
     int inclusive;
 };
-hipError_t launch_scan(int dt, const ScanArgs &a, int grid, hipStream_t s);
+hipError_t launch_scan(int dt, const ScanArgs &a, bool vec, int grid, hipStream_t s);
 
 // Arguments of the local k-input fan-in combine: dst = op(src0, src1, ..., src_{k-1}).
 constexpr int kMaxFanin = 16;

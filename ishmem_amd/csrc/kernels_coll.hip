@@ -59,48 +59,81 @@ __global__ __launch_bounds__(kBlock) void collect_kernel(CollectArgs a)
 // Prefix sum.  Phase 1: member c owns chunk c; for each element it folds the members' values in
 // team order and stores every member k's prefix into its own scratch row k (write-through).
 // Phase 2 (after the mid barrier): each member pulls its row of every chunk into dest.
-template <typename T>
+// Items are 16-B vectors when every base is 16-B aligned (chunk sizes are multiples of 64
+// elements); the < 16 leftover elements of the last chunk go element by element.  For P in
+// {2, 4, 8} the P loads of an item are all issued before the first store (compile-time register
+// staging), so a tile costs one round trip instead of P.
+template <typename T, typename I>
+__device__ __forceinline__ I scan_add(const I &a, const I &b)
+{
+    return op1<T, ISHMEMI_OP_SUM>(a, b);
+}
+
+template <typename T, typename I, int P>
+__device__ __forceinline__ void scan_item_fold(const ScanArgs &a, const char *const *base, char *const *row,
+                                               uint32_t off, int p, int me, bool ok_item)
+{
+    if (!ok_item) return;
+    I acc{};
+    if constexpr (P > 0) {
+        I x[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) x[k] = cload<I>(make_rsrc(base[k]), off);
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const I incl = k == 0 ? x[0] : scan_add<T, I>(acc, x[k]);  // first term kept (sign of 0)
+            wt_store(make_rsrc(row[k]), off, a.inclusive ? incl : acc);
+            acc = incl;
+        }
+    } else {
+        for (int k = 0; k < p; ++k) {
+            const I x = cload<I>(make_rsrc(base[k]), off);
+            const I incl = k == 0 ? x : scan_add<T, I>(acc, x);
+            wt_store(make_rsrc(row[k]), off, a.inclusive ? incl : acc);
+            acc = incl;
+        }
+    }
+    (void) me;
+}
+
+template <typename T, bool VEC, int P>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
 {
+    using I = std::conditional_t<VEC, Vec<T>, T>;
+    constexpr uint64_t E = sizeof(I) / sizeof(T);
+    constexpr int H = (P == 8 || P == 0) ? 2 : kUnroll;
+    constexpr uint64_t kT = (uint64_t) kBlock * H;
     const int tid = threadIdx.x, b = blockIdx.x;
     const uint64_t G = gridDim.x;
-    const int p = a.p, me = a.me;
+    const int p = P > 0 ? P : a.p, me = a.me;
     const uint64_t ipc = a.items_per_chunk;
     bool ok = pe_barrier<false>(a, kPhaseStart, b);
     if (ok) {
         const uint64_t cs = min((uint64_t) me * ipc, a.nelems), ce = min(cs + ipc, a.nelems);
-        for (uint64_t t0 = cs + (uint64_t) b * kTile; t0 < ce; t0 += G * kTile) {
-            T acc[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) acc[u] = T(0);
+        const uint64_t nI = (ce - cs) / E;
+        for (uint64_t t0 = (uint64_t) b * kT; t0 < nI; t0 += G * kT) {
+            const char *base[kMaxPes];
+            char *row[kMaxPes];
             for (int k = 0; k < p; ++k) {
-                T x[kUnroll];
-                const char *base = uniform_ptr(a.src[k] + t0 * sizeof(T));
-                if (k == me) {
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) {
-                        const uint64_t e = (uint64_t) u * kBlock + tid;
-                        if (t0 + e < ce) x[u] = ((const T *) base)[e];
-                    }
-                } else {
-                    const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) {
-                        const uint64_t e = (uint64_t) u * kBlock + tid;
-                        if (t0 + e < ce) x[u] = cload<T>(r, (uint32_t) (e * sizeof(T)));
-                    }
-                }
-                // Row k of the scratch holds member k's result for this chunk.
-                const __amdgpu_buffer_rsrc_t wr =
-                    make_rsrc(uniform_ptr(a.scratch[me] + ((uint64_t) k * ipc + (t0 - cs)) * sizeof(T)));
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const uint64_t e = (uint64_t) u * kBlock + tid;
-                    const T incl = k == 0 ? x[u] : op1<T, ISHMEMI_OP_SUM>(acc[u], x[u]);  // keeps -0.0
-                    if (t0 + e < ce) wt_store(wr, (uint32_t) (e * sizeof(T)), a.inclusive ? incl : acc[u]);
-                    acc[u] = incl;
-                }
+                base[k] = uniform_ptr(a.src[k] + (cs + t0 * E) * sizeof(T));
+                row[k] = (char *) uniform_ptr(a.scratch[me] + ((uint64_t) k * ipc + t0 * E) * sizeof(T));
             }
+#pragma unroll
+            for (int u = 0; u < H; ++u) {
+                const uint64_t e = (uint64_t) u * kBlock + tid;
+                scan_item_fold<T, I, P>(a, base, row, (uint32_t) (e * sizeof(I)), p, me, t0 + e < nI);
+            }
+        }
+        const uint64_t tail = (ce - cs) - nI * E;  // < E elements, last chunk only
+        if (tail && b == (int) ((nI / kT) % G) && (uint64_t) tid < tail) {
+            const uint64_t el = nI * E + tid;
+            const char *base[kMaxPes];
+            char *row[kMaxPes];
+            for (int k = 0; k < p; ++k) {
+                base[k] = uniform_ptr(a.src[k] + (cs + nI * E) * sizeof(T));
+                row[k] = (char *) uniform_ptr(a.scratch[me] + ((uint64_t) k * ipc + nI * E) * sizeof(T));
+            }
+            scan_item_fold<T, T, 0>(a, base, row, (uint32_t) ((el - nI * E) * sizeof(T)), p, me, true);
         }
     }
     ok = ok && pe_barrier<true>(a, kPhaseMid, b);
@@ -108,21 +141,28 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
         for (int k = 0; k < p; ++k) {
             const int c = (me + b + k) % p;  // rotated over the members' scratch (links)
             const uint64_t cs = min((uint64_t) c * ipc, a.nelems), ce = min(cs + ipc, a.nelems);
-            for (uint64_t t0 = cs + (uint64_t) b * kTile; t0 < ce; t0 += G * kTile) {
-                const char *base = uniform_ptr(a.scratch[c] + ((uint64_t) me * ipc + (t0 - cs)) * sizeof(T));
-                const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
-                T x[kUnroll];
+            const uint64_t nI = (ce - cs) / E;
+            const char *rowbase = a.scratch[c] + (uint64_t) me * ipc * sizeof(T);
+            for (uint64_t t0 = (uint64_t) b * kT; t0 < nI; t0 += G * kT) {
+                const __amdgpu_buffer_rsrc_t r = make_rsrc(uniform_ptr(rowbase + t0 * E * sizeof(T)));
+                I x[H];
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
+                for (int u = 0; u < H; ++u) {
                     const uint64_t e = (uint64_t) u * kBlock + tid;
-                    if (t0 + e < ce) x[u] = cload<T>(r, (uint32_t) (e * sizeof(T)));
+                    if (t0 + e < nI) x[u] = cload<I>(r, (uint32_t) (e * sizeof(I)));
                 }
-                T *dp = (T *) (a.dst + t0 * sizeof(T));
+                I *dp = (I *) (a.dst + (cs + t0 * E) * sizeof(T));
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
+                for (int u = 0; u < H; ++u) {
                     const uint64_t e = (uint64_t) u * kBlock + tid;
-                    if (t0 + e < ce) dp[e] = x[u];
+                    if (t0 + e < nI) nt_store(dp + e, x[u]);
                 }
+            }
+            const uint64_t tail = (ce - cs) - nI * E;
+            if (tail && b == (int) ((nI / kT) % G) && (uint64_t) tid < tail) {
+                const uint64_t el = nI * E + tid;
+                const __amdgpu_buffer_rsrc_t r = make_rsrc(uniform_ptr(rowbase + nI * E * sizeof(T)));
+                ((T *) (a.dst + cs * sizeof(T)))[el] = cload<T>(r, (uint32_t) (tid * sizeof(T)));
             }
         }
     }
@@ -147,15 +187,30 @@ hipError_t launch_collect(const CollectArgs &a, int grid, hipStream_t s)
     return launch_res(collect_kernel<1>, a, grid, s);
 }
 
-hipError_t launch_scan(int dt, const ScanArgs &a, int grid, hipStream_t s)
+template <typename T>
+hipError_t scan_t(const ScanArgs &a, bool vec, int grid, hipStream_t s)
+{
+    if (!vec) {
+        if (a.p == 2) return launch_res(scan_kernel<T, false, 2>, a, grid, s);
+        if (a.p == 4) return launch_res(scan_kernel<T, false, 4>, a, grid, s);
+        if (a.p == 8) return launch_res(scan_kernel<T, false, 8>, a, grid, s);
+        return launch_res(scan_kernel<T, false, 0>, a, grid, s);
+    }
+    if (a.p == 2) return launch_res(scan_kernel<T, true, 2>, a, grid, s);
+    if (a.p == 4) return launch_res(scan_kernel<T, true, 4>, a, grid, s);
+    if (a.p == 8) return launch_res(scan_kernel<T, true, 8>, a, grid, s);
+    return launch_res(scan_kernel<T, true, 0>, a, grid, s);
+}
+
+hipError_t launch_scan(int dt, const ScanArgs &a, bool vec, int grid, hipStream_t s)
 {
     switch (dt) {  // sum wraps on the unsigned type of the same width (two's complement)
-        case ISHMEMI_DT_INT8: case ISHMEMI_DT_UINT8: return launch_res(scan_kernel<uint8_t>, a, grid, s);
-        case ISHMEMI_DT_INT16: case ISHMEMI_DT_UINT16: return launch_res(scan_kernel<uint16_t>, a, grid, s);
-        case ISHMEMI_DT_INT32: case ISHMEMI_DT_UINT32: return launch_res(scan_kernel<uint32_t>, a, grid, s);
-        case ISHMEMI_DT_INT64: case ISHMEMI_DT_UINT64: return launch_res(scan_kernel<uint64_t>, a, grid, s);
-        case ISHMEMI_DT_FLOAT: return launch_res(scan_kernel<float>, a, grid, s);
-        case ISHMEMI_DT_DOUBLE: return launch_res(scan_kernel<double>, a, grid, s);
+        case ISHMEMI_DT_INT8: case ISHMEMI_DT_UINT8: return scan_t<uint8_t>(a, vec, grid, s);
+        case ISHMEMI_DT_INT16: case ISHMEMI_DT_UINT16: return scan_t<uint16_t>(a, vec, grid, s);
+        case ISHMEMI_DT_INT32: case ISHMEMI_DT_UINT32: return scan_t<uint32_t>(a, vec, grid, s);
+        case ISHMEMI_DT_INT64: case ISHMEMI_DT_UINT64: return scan_t<uint64_t>(a, vec, grid, s);
+        case ISHMEMI_DT_FLOAT: return scan_t<float>(a, vec, grid, s);
+        case ISHMEMI_DT_DOUBLE: return scan_t<double>(a, vec, grid, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -586,10 +586,11 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
             a.nelems = m;
             a.items_per_chunk = items_per_chunk(m, t.size);
             a.inclusive = inclusive;
-            const uint64_t tile = (uint64_t) kBlock * kUnroll;
+            const bool vec = (((uintptr_t) dst | (uintptr_t) src | (uintptr_t) s.staging) & 15) == 0;
+            const uint64_t tile = (uint64_t) kBlock * 2 * (vec ? 16 / es : 1);
             const int grid = (int) std::max<uint64_t>(
                 1, std::min<uint64_t>((a.items_per_chunk + tile - 1) / tile, s.max_blocks));
-            HIP_TRY(launch_scan(dt, a, grid, st));
+            HIP_TRY(launch_scan(dt, a, vec, grid, st));
         }
     }
     if (mark_stream(s, st)) return 1;

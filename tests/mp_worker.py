@@ -423,6 +423,17 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                                      f"{int(np.sum(got.view(np.uint8) != ref.view(np.uint8)))} bytes differ")
                 ish.ishmem_free(d_b)
                 ish.ishmem_free(s_b)
+            # element-granular path: 4-B aligned (not 16-B) buffers, odd length
+            n = 50_001
+            ins = [oracle.fill_random(DT["int32"], 650 + j, n) for j in range(npes)]
+            s_b, d_b = heap(n + 8, DT["int32"]), heap(n + 8, DT["int32"])
+            hip.upload(s_b + 4, ins[pe])
+            for inc in (True, False):
+                r = ish.scan("int32", inc, d_b + 12, s_b + 4, n)
+                if r or not _bits_equal(hip.download(d_b + 12, n, np.int32), oracle.scan_fold(DT["int32"], ins, pe, inc)):
+                    fails.append(f"pe{pe} misaligned scan inc={inc} wrong {ish.last_error()}")
+            ish.ishmem_free(d_b)
+            ish.ishmem_free(s_b)
             # several staging-sized segments (ISHMEM_STAGING_SIZE small in the test env)
             n = 3 * (ish.get_param("staging_bytes") // 4) + 17
             ins = [oracle.fill_random(DT["int32"], 700 + j, n) for j in range(npes)]
