@@ -174,7 +174,9 @@ void *ishmemi_c_device_ctx(void);
 /* ---- diagnostics / parameters ----------------------------------------------------------------
  * ishmemi_c_set_param names: "max_blocks" (workgroups per collective launch, <= 1024),
  * "ll_max_bytes" (one-hop granule path threshold, <= 65536), "timeout_ms" (bound on every
- * device-side spin), "debug".  "max_blocks" and "ll_max_bytes" shape every multi-PE launch: init
+ * device-side spin), "stream_order" (1: collectives issued on different streams are ordered by
+ * the library in call order, ~2 us per call; 0, the default: the caller orders them, as the
+ * reference requires), "debug".  "max_blocks" and "ll_max_bytes" shape every multi-PE launch: init
  * agrees on them (minimum over the PEs); a later set_param must be made with the same value on
  * every PE.  ishmemi_c_get_param also reports "staging_bytes" and "flags_fine_grained". */
 const char *ishmemi_c_last_error(void);

@@ -39,7 +39,7 @@ struct ReduceArgs {
     uint64_t tail;    // scalar elements after the body
     uint64_t items_per_chunk;
     uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
-    uint32_t epoch;
+    uint32_t *ep_ctr;  // team's kernel-epoch counter: [0] last epoch, [1] workgroups done
     int p, me;
 };
 
@@ -58,7 +58,7 @@ struct LLArgs {
     int *ret;
     uint64_t nbytes;
     uint64_t timeout_ticks;
-    uint32_t epoch;
+    uint32_t *ep_ctr;  // team's kernel-epoch counter: [0] last epoch, [1] workgroups done
     int p, me;
 };
 hipError_t launch_ll(int op, int dt, const LLArgs &a, hipStream_t s);
@@ -75,7 +75,7 @@ struct CollectArgs {
     uint32_t *err;
     int *ret;
     uint64_t timeout_ticks;
-    uint32_t epoch;
+    uint32_t *ep_ctr;  // team's kernel-epoch counter: [0] last epoch, [1] workgroups done
     int p, me;
     int unit;  // bytes per item: 16, 4 or 1 (largest dividing every address and length)
 };
@@ -92,7 +92,7 @@ struct ScanArgs {
     int *ret;
     uint64_t nelems, items_per_chunk;
     uint64_t timeout_ticks;
-    uint32_t epoch;
+    uint32_t *ep_ctr;  // team's kernel-epoch counter: [0] last epoch, [1] workgroups done
     int p, me;
     int inclusive;
 };

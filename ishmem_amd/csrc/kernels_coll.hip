@@ -20,7 +20,8 @@ __global__ __launch_bounds__(kBlock) void collect_kernel(CollectArgs a)
     using Item = std::conditional_t<U == 16, Vec<uint32_t>, std::conditional_t<U == 4, uint32_t, uint8_t>>;
     const int tid = threadIdx.x, b = blockIdx.x;
     const uint64_t G = gridDim.x;
-    bool ok = pe_barrier<false>(a, kPhaseStart, b);
+    const uint32_t ep = kernel_epoch(a);
+    bool ok = pe_barrier<false>(a, ep, kPhaseStart, b);
     if (ok) {
         for (int k = 0; k < a.p; ++k) {
             const int j = (a.me + (b + k)) % a.p;
@@ -52,8 +53,9 @@ __global__ __launch_bounds__(kBlock) void collect_kernel(CollectArgs a)
         }
     }
     // No member returns while a peer may still read its source.
-    ok = ok && pe_barrier<false>(a, kPhaseEnd, b);
+    ok = ok && pe_barrier<false>(a, ep, kPhaseEnd, b);
     if (b == 0 && tid == 0 && a.ret) *a.ret = ok ? 0 : 1;
+    kernel_epoch_done(a, ep);
 }
 
 // Prefix sum.  Phase 1: member c owns chunk c; for each element it folds the members' values in
@@ -107,7 +109,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
     const uint64_t G = gridDim.x;
     const int p = P > 0 ? P : a.p, me = a.me;
     const uint64_t ipc = a.items_per_chunk;
-    bool ok = pe_barrier<false>(a, kPhaseStart, b);
+    const uint32_t ep = kernel_epoch(a);
+    bool ok = pe_barrier<false>(a, ep, kPhaseStart, b);
     if (ok) {
         const uint64_t cs = min((uint64_t) me * ipc, a.nelems), ce = min(cs + ipc, a.nelems);
         const uint64_t nI = (ce - cs) / E;
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
             scan_item_fold<T, T, 0>(a, base, row, (uint32_t) ((el - nI * E) * sizeof(T)), p, me, true);
         }
     }
-    ok = ok && pe_barrier<true>(a, kPhaseMid, b);
+    ok = ok && pe_barrier<true>(a, ep, kPhaseMid, b);
     if (ok) {
         for (int k = 0; k < p; ++k) {
             const int c = (me + b + k) % p;  // rotated over the members' scratch (links)
@@ -166,8 +169,9 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
             }
         }
     }
-    ok = ok && pe_barrier<false>(a, kPhaseEnd, b);
+    ok = ok && pe_barrier<false>(a, ep, kPhaseEnd, b);
     if (b == 0 && tid == 0 && a.ret) *a.ret = ok ? 0 : 1;
+    kernel_epoch_done(a, ep);
 }
 
 template <typename K, typename A>

@@ -140,6 +140,34 @@ __device__ __forceinline__ void wt_store(__amdgpu_buffer_rsrc_t r, uint32_t off,
     else __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, v), r, off, 0, kSysCoherent);
 }
 
+// Kernel epochs live on the device: every workgroup of a launch reads the team's counter at
+// its start (epoch = counter + 1, 0 skipped: it is the flags' initial value) and the last
+// workgroup to finish stores the new value.  Collectives of a team are stream-ordered, so the
+// next launch sees it; a captured hipGraph therefore replays with fresh epochs every time.
+template <typename A>
+__device__ __forceinline__ uint32_t kernel_epoch(const A &a)
+{
+    __shared__ uint32_t s_ep;
+    if (threadIdx.x == 0) {
+        uint32_t e = __hip_atomic_load(a.ep_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+        s_ep = e == 0 ? 1u : e;
+    }
+    __syncthreads();
+    return s_ep;
+}
+
+template <typename A>
+__device__ __forceinline__ void kernel_epoch_done(const A &a, uint32_t ep)
+{
+    if (threadIdx.x == 0) {
+        if (__hip_atomic_fetch_add(a.ep_ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
+            gridDim.x - 1) {
+            __hip_atomic_store(a.ep_ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.ep_ctr, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t *flag_slot(uint32_t *base, int phase, int block)
 {
     return base + ((size_t) phase * kMaxBlocks + (size_t) block) * kMaxPes;
@@ -152,7 +180,7 @@ __device__ __forceinline__ uint32_t *flag_slot(uint32_t *base, int phase, int bl
 // holds the epoch (wrap-safe compare).  Called by ALL threads of the block; returns false on
 // timeout (recorded in *err) so the caller can drain instead of hanging the GPU.
 template <bool RELEASE, typename A>
-__device__ bool pe_barrier(const A &a, int phase, int block)
+__device__ bool pe_barrier(const A &a, uint32_t ep, int phase, int block)
 {
     __shared__ int s_ok;
     // Every storing wave drains its stores, then one wave publishes (Guideline 16, R1).
@@ -174,7 +202,7 @@ __device__ bool pe_barrier(const A &a, int phase, int block)
         if (lane == 0) {
             for (int j = 0; j < p; ++j) {
                 if (j == me) continue;
-                __hip_atomic_store(flag_slot(a.peer_flags[j], phase, block) + me, a.epoch,
+                __hip_atomic_store(flag_slot(a.peer_flags[j], phase, block) + me, ep,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
@@ -186,7 +214,7 @@ __device__ bool pe_barrier(const A &a, int phase, int block)
             if (!done) {
                 const uint32_t v =
                     __hip_atomic_load(row + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                done = (int32_t) (v - a.epoch) >= 0;
+                done = (int32_t) (v - ep) >= 0;
             }
             if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
                 timed_out = true;
@@ -282,7 +310,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
     const uint64_t G = gridDim.x;
     const int p = a.p, me = a.me;
     const uint64_t head_bytes = VEC ? a.head * sizeof(T) : 0;
-    bool ok = pe_barrier<false>(a, kPhaseStart, b);
+    const uint32_t ep = kernel_epoch(a);
+    bool ok = pe_barrier<false>(a, ep, kPhaseStart, b);
 
     // ---- reduce-scatter: fold chunk `me` of every member's source, canonical team order ----
     // The LOAD order is rotated by workgroup index (rot = b mod p), so at any instant the
@@ -360,7 +389,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
         }
     }
 
-    ok = ok && pe_barrier<true>(a, kPhaseMid, b);
+    ok = ok && pe_barrier<true>(a, ep, kPhaseMid, b);
 
     // ---- all-gather: pull every other member's reduced chunk from its dest ----
     if (ok) {
@@ -401,8 +430,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
     }
 
     // ---- end: peers have finished pulling from my dest before anyone returns ----
-    ok = ok && pe_barrier<false>(a, kPhaseEnd, b);
+    ok = ok && pe_barrier<false>(a, ep, kPhaseEnd, b);
     if (b == 0 && tid == 0 && a.ret) *a.ret = ok ? 0 : 1;
+    kernel_epoch_done(a, ep);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -483,8 +513,9 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
     const uint64_t item = (uint64_t) blockIdx.x * kBlock + threadIdx.x;
     const uint64_t nitems = (a.nbytes + 7) / 8;
     const int p = a.p, me = a.me;
-    const uint64_t par = a.epoch & 1u;
-    const uint64_t tag = (uint64_t) a.epoch << 32;
+    const uint32_t ep = kernel_epoch(a);
+    const uint64_t par = ep & 1u;
+    const uint64_t tag = (uint64_t) ep << 32;
     bool ok = true;
     if (item < nitems) {
         const uint64_t off = item * 8;
@@ -509,7 +540,7 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
                 for (;;) {
                     h0 = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     h1 = __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if ((h0 >> 32) == a.epoch && (h1 >> 32) == a.epoch) break;
+                    if ((h0 >> 32) == ep && (h1 >> 32) == ep) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
                         ok = false;
                         __hip_atomic_fetch_or(a.err, 1u << 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -527,6 +558,7 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
         }
     }
     if (a.ret && blockIdx.x == 0 && threadIdx.x == 0) *a.ret = ok ? 0 : 1;
+    kernel_epoch_done(a, ep);
 }
 
 template <typename T, int OP>
@@ -541,8 +573,10 @@ hipError_t ll_t(const LLArgs &a, hipStream_t s)
 // Standalone team barrier (ishmem_team_sync / barrier_all analogue): one workgroup.
 __global__ __launch_bounds__(kBlock) void team_sync_kernel(ReduceArgs a)
 {
-    const bool ok = pe_barrier<false>(a, kPhaseSync, 0);
+    const uint32_t ep = kernel_epoch(a);
+    const bool ok = pe_barrier<false>(a, ep, kPhaseSync, 0);
     if (threadIdx.x == 0 && a.ret) *a.ret = ok ? 0 : 1;
+    kernel_epoch_done(a, ep);
 }
 
 // Canonical kernel type: MIN/MAX keep the signedness, every other integer op folds on the

@@ -82,7 +82,6 @@ struct Team {
     bool valid = false;
     int start = 0, stride = 1, size = 1;  // in world PEs (src/teams.h:56-76)
     int my_idx = -1;                      // my index in the team, -1 if not a member
-    uint32_t epoch = 0;                   // last epoch used by a collective of this team
 };
 
 struct PeRecord {
@@ -115,6 +114,7 @@ struct State {
     uint32_t *err_dev = nullptr;
     ishmemi_c_device_ctx_t *dctx = nullptr;  // device copy of the device-API context
     uint32_t *dev_epochs = nullptr;
+    uint32_t *kern_ep = nullptr;  // [team][2] kernel-epoch counters of the host-launched kernels
 
     char *team_scratch = nullptr;  // small symmetric buffer for team-management collectives
     char *staging = nullptr;  // symmetric staging region for non-heap / host buffers
@@ -124,7 +124,12 @@ struct State {
     // for it, so epochs, flag rows and the staging region are used in call order.
     hipStream_t last_stream = nullptr;
     bool last_stream_set = false;
+    bool stream_order = false;
     hipEvent_t order_ev = nullptr;
+    // Completion of the last use of the staging region (staged pipeline or scan scratch); the
+    // next user waits on it, whatever stream it runs on.
+    hipEvent_t staging_ev = nullptr;
+    bool staging_used = false;
     hipEvent_t ev_in[2] = {}, ev_red[2] = {}, ev_out[2] = {};
 
     Team teams[kMaxTeams];
@@ -279,8 +284,7 @@ int team_args(State &s, int team, ReduceArgs &a, std::string &why)
             return 1;
         }
     }
-    if (++t.epoch == 0) t.epoch = 1;
-    a.epoch = t.epoch;
+    a.ep_ctr = s.kern_ep + 2 * team;
     return 0;
 }
 
@@ -339,27 +343,56 @@ bool ll_eligible(const State &s, const Team &t, const void *dst, const void *src
 // Collectives of one PE run in the order they were called, whatever streams they were enqueued
 // on (the flag protocol pairs the k-th collective of a team on every PE; the staging region is
 // shared).  Same stream as last time: nothing to do.
-// The switch is handled when it happens: an event recorded on the previous stream, waited on by
-// the new one (no per-call event: a recorded event costs microseconds of device time).  If the
-// previous stream has been destroyed since, the record fails and the device is drained instead.
+// Cross-stream ordering (ISHMEM_STREAM_ORDER=1 / set_param "stream_order"): every collective
+// records one device-scope event after its launches (mark_stream) and a collective enqueued on
+// another stream than the previous one first waits on it (order_stream).  The event is the
+// library's, so the earlier stream may since have been destroyed.  Off by default: like the
+// reference (collectives of a team are not concurrency-safe, src/teams.h:29-38), the caller
+// orders collectives it issues on different streams; the per-call event costs ~2 us of device
+// time per collective.  The staging region is always protected (staging_ev).
+bool capturing(hipStream_t st)
+{
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+        (void) hipGetLastError();
+        return false;
+    }
+    return cs != hipStreamCaptureStatusNone;
+}
+
+// Work captured into a hipGraph runs when the graph is launched: ordering it against other
+// collectives is the caller's (launch order), so captured calls neither wait nor mark.
 int order_stream(State &s, hipStream_t st)
 {
-    if (s.last_stream_set && s.last_stream != st) {
-        if (!s.order_ev) HIP_TRY(hipEventCreateWithFlags(&s.order_ev, hipEventDisableTiming));
-        if (hipEventRecord(s.order_ev, s.last_stream) == hipSuccess) {
-            HIP_TRY(hipStreamWaitEvent(st, s.order_ev, 0));
-        } else {
-            (void) hipGetLastError();
-            HIP_TRY(hipDeviceSynchronize());
-        }
-    }
+    if (!s.stream_order) return 0;
+    if (s.last_stream_set && s.last_stream != st && !capturing(st))
+        HIP_TRY(hipStreamWaitEvent(st, s.order_ev, 0));
     return 0;
 }
 
 int mark_stream(State &s, hipStream_t st)
 {
+    if (!s.stream_order || capturing(st)) return 0;
+    if (!s.order_ev)
+        HIP_TRY(hipEventCreateWithFlags(&s.order_ev, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIP_TRY(hipEventRecord(s.order_ev, st));
     s.last_stream = st;
     s.last_stream_set = true;
+    return 0;
+}
+
+int staging_acquire(State &s, hipStream_t st)
+{
+    if (s.staging_used && !capturing(st)) HIP_TRY(hipStreamWaitEvent(st, s.staging_ev, 0));
+    return 0;
+}
+
+int staging_release(State &s, hipStream_t st)
+{
+    if (capturing(st)) return 0;
+    if (!s.staging_ev) HIP_TRY(hipEventCreateWithFlags(&s.staging_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(s.staging_ev, st));
+    s.staging_used = true;
     return 0;
 }
 
@@ -382,8 +415,7 @@ int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, si
     a.ret = ret;
     a.nbytes = bytes;
     a.timeout_ticks = (uint64_t) s.timeout_ms * 100000ull;
-    if (++t.epoch == 0) t.epoch = 1;
-    a.epoch = t.epoch;
+    a.ep_ctr = s.kern_ep + 2 * team;
     a.p = t.size;
     a.me = t.my_idx;
     HIP_TRY(launch_ll(op, dt, a, st));
@@ -441,6 +473,7 @@ int reduce_staged(State &s, int team, int op, int dt, void *dst, const void *src
             HIP_TRY(hipEventCreateWithFlags(&s.ev_out[i], hipEventDisableTiming));
         }
     }
+    if (staging_acquire(s, st)) return 1;
     HIP_TRY(hipEventRecord(s.ev_red[0], st));  // copy-ins start after the caller's prior work
     HIP_TRY(hipStreamWaitEvent(s.copy_in, s.ev_red[0], 0));
     bool used[2] = {false, false};
@@ -468,7 +501,7 @@ int reduce_staged(State &s, int team, int op, int dt, void *dst, const void *src
     }
     for (int sl = 0; sl < 2; ++sl)  // the caller's stream completes only after every copy-out
         if (used[sl]) HIP_TRY(hipStreamWaitEvent(st, s.ev_out[sl], 0));
-    return 0;
+    return staging_release(s, st);
 }
 
 // ---------------- fcollect / collect / scan --------------------------
@@ -483,7 +516,7 @@ int fill_team_sync_args(State &s, int team, A &a, std::string &why)
     for (int j = 0; j < r.p; ++j) a.peer_flags[j] = r.peer_flags[j];
     a.err = r.err;
     a.timeout_ticks = r.timeout_ticks;
-    a.epoch = r.epoch;
+    a.ep_ctr = r.ep_ctr;
     a.p = r.p;
     a.me = r.me;
     return 0;
@@ -569,7 +602,7 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
         const uint64_t ipc_max = ((s.staging_bytes / es) / (uint64_t) t.size) & ~uint64_t(63);
         const uint64_t seg = ipc_max * (uint64_t) t.size;
         if (ipc_max == 0) return fail("scan: staging region too small for this team");
-        if (order_stream(s, st)) return 1;
+        if (order_stream(s, st) || staging_acquire(s, st)) return 1;
         for (uint64_t off = 0; off < n; off += seg) {
             const uint64_t m = std::min<uint64_t>(seg, n - off);
             ScanArgs a;
@@ -592,6 +625,7 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
                 1, std::min<uint64_t>((a.items_per_chunk + tile - 1) / tile, s.max_blocks));
             HIP_TRY(launch_scan(dt, a, vec, grid, st));
         }
+        if (staging_release(s, st)) return 1;
     }
     if (mark_stream(s, st)) return 1;
     if (blocking) {
@@ -708,6 +742,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
                                          std::max<long long>(0, env_ll("ISHMEM_LL_MAX_BYTES", (long long) kLLDefaultBytes)));
     s.debug = (int) env_ll("ISHMEM_DEBUG", 0);
+    s.stream_order = env_ll("ISHMEM_STREAM_ORDER", 0) != 0;
     s.staging_bytes = (parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20) + kHeapAlign - 1) &
                       ~(size_t) (kHeapAlign - 1);
 
@@ -827,6 +862,12 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.team_scratch = (char *) heap_alloc(s, kHeapAlign, kHeapAlign);
     if (!s.team_scratch) return 1;
     HIP_TRY(hipMalloc((void **) &s.dctx, sizeof(ishmemi_c_device_ctx_t)));
+    if (hipExtMallocWithFlags((void **) &s.kern_ep, 2 * kMaxTeams * sizeof(uint32_t), hipDeviceMallocUncached) !=
+        hipSuccess) {
+        (void) hipGetLastError();
+        HIP_TRY(hipMalloc((void **) &s.kern_ep, 2 * kMaxTeams * sizeof(uint32_t)));
+    }
+    HIP_TRY(hipMemset(s.kern_ep, 0, 2 * kMaxTeams * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void **) &s.dev_epochs, kMaxTeams * sizeof(uint32_t)));
     HIP_TRY(hipMemset(s.dev_epochs, 0, kMaxTeams * sizeof(uint32_t)));
     if (sync_device_ctx(s)) return 1;
@@ -906,8 +947,12 @@ int ishmemi_c_finalize(void)
     (void) hipHostFree(s.err_host);
     (void) hipFree(s.dctx);
     (void) hipFree(s.dev_epochs);
+    (void) hipFree(s.kern_ep);
+    s.kern_ep = nullptr;
     if (s.order_ev) (void) hipEventDestroy(s.order_ev);
-    s.order_ev = nullptr;
+    if (s.staging_ev) (void) hipEventDestroy(s.staging_ev);
+    s.order_ev = s.staging_ev = nullptr;
+    s.staging_used = false;
     s.last_stream = nullptr;
     s.last_stream_set = false;
     s.dctx = nullptr;
@@ -1075,6 +1120,7 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
             hipMemset(dev_flags(s.flags) + (size_t) slot * kDevFlagWordsPerTeam, 0,
                       kDevFlagWordsPerTeam * 4) != hipSuccess ||
             hipMemset(s.dev_epochs + slot, 0, sizeof(uint32_t)) != hipSuccess ||
+            hipMemset(s.kern_ep + 2 * slot, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
             hipMemset(ll_ring(s.flags, slot), 0, kLLTeamBytes) != hipSuccess)
             return fail("team_split_strided: flag reset failed");
         if (sync_device_ctx(s)) return 1;
@@ -1240,6 +1286,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     const std::string n = name ? name : "";
     if (n == "max_blocks") s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, value));
     else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
+    else if (n == "stream_order") s.stream_order = value != 0;
     else if (n == "ll_max_bytes") s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes, std::max<long long>(0, value));
     else if (n == "debug") s.debug = (int) value;
     else return fail("set_param: unknown parameter " + n);
@@ -1252,6 +1299,7 @@ long long ishmemi_c_get_param(const char *name)
     const std::string n = name ? name : "";
     if (n == "max_blocks") return s.max_blocks;
     if (n == "timeout_ms") return s.timeout_ms;
+    if (n == "stream_order") return s.stream_order ? 1 : 0;
     if (n == "ll_max_bytes") return s.ll_max_bytes;
     if (n == "debug") return s.debug;
     if (n == "flags_fine_grained") return s.flags_fine_grained ? 1 : 0;

@@ -132,3 +132,41 @@ class Event:
                 lib().hipEventDestroy(ctypes.c_void_p(self.h))
         except Exception:
             pass
+
+
+class Graph:
+    """Stream capture into a hipGraph: `with Graph(stream) as g: <enqueue on stream>`, then
+    g.launch(stream) replays the captured work."""
+
+    def __init__(self, stream: int) -> None:
+        self.stream = stream
+        self.graph = None
+        self.exec = None
+
+    def __enter__(self) -> "Graph":
+        # hipStreamCaptureModeThreadLocal = 1
+        _check(lib().hipStreamBeginCapture(ctypes.c_void_p(self.stream), ctypes.c_int(1)), "hipStreamBeginCapture")
+        return self
+
+    def __exit__(self, *exc) -> None:
+        g = ctypes.c_void_p()
+        _check(lib().hipStreamEndCapture(ctypes.c_void_p(self.stream), ctypes.byref(g)), "hipStreamEndCapture")
+        self.graph = g.value
+        if exc[0] is None:
+            ge = ctypes.c_void_p()
+            _check(lib().hipGraphInstantiate(ctypes.byref(ge), ctypes.c_void_p(self.graph), None, None,
+                                             ctypes.c_size_t(0)), "hipGraphInstantiate")
+            self.exec = ge.value
+
+    def launch(self, stream: int | None = None) -> None:
+        _check(lib().hipGraphLaunch(ctypes.c_void_p(self.exec), ctypes.c_void_p(self.stream if stream is None else stream)),
+               "hipGraphLaunch")
+
+    def __del__(self) -> None:
+        try:
+            if self.exec:
+                lib().hipGraphExecDestroy(ctypes.c_void_p(self.exec))
+            if self.graph:
+                lib().hipGraphDestroy(ctypes.c_void_p(self.graph))
+        except Exception:
+            pass

@@ -179,7 +179,8 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
         if "streams" in scenarios:
             # Back-to-back collectives on different streams with no host synchronisation between
             # them (each must follow the previous one: same epochs / flag rows / staging on every
-            # PE), the last stream destroyed before a blocking call.
+            # PE), the last stream destroyed before a blocking call.  ISHMEM_STREAM_ORDER on.
+            ish.set_param("stream_order", 1)
             n = 70_000
             ins = [[oracle.fill_random(DT["int32"], 300 + 10 * r + j, n) for j in range(npes)] for r in range(4)]
             s_b = [heap(n, DT["int32"]) for _ in range(4)]
@@ -206,6 +207,48 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 hip.stream_destroy(st_)
             for b in s_b + d_b:
                 ish.ishmem_free(b)
+            ish.set_param("stream_order", 0)
+
+        if "graph" in scenarios:
+            # A captured hipGraph of on_stream collectives (LL path, RS + AG path, fcollect,
+            # inscan) replayed several times: kernel epochs come from the device-side counter,
+            # so every replay synchronises afresh.  Inputs change between replays.
+            st_ = hip.stream_create()
+            n_small, n_big = 600, 300_000
+            s1, d1 = heap(n_small, DT["double"]), heap(n_small, DT["double"])
+            s2, d2 = heap(n_big, DT["float"]), heap(n_big, DT["float"])
+            fc = ish.ishmem_malloc(4096 * npes)
+            sc = heap(n_big, DT["int32"])
+            ret = ish.ishmem_malloc(4)
+            ish.ishmem_barrier_all()
+            with hip.Graph(st_) as g:
+                ish.ishmemx_double_max_reduce_on_stream(d1, s1, n_small, ret, st_)
+                ish.ishmemx_float_sum_reduce_on_stream(d2, s2, n_big, ret, st_)
+                ish.fcollect_on_stream(fc, s1, 4096, ret, st_)
+                ish.lib().ishmemi_c_scan_on_stream(0, DT["int32"], 1, sc, s2, n_big, ret, st_)
+            for rep in range(4):
+                a = [oracle.fill_random(DT["double"], 900 + 10 * rep + j, n_small) for j in range(npes)]
+                b = [oracle.fill_random(DT["float"], 950 + 10 * rep + j, n_big) for j in range(npes)]
+                hip.upload(s1, a[pe])
+                hip.upload(s2, b[pe])
+                hip.memset(ret, 0xFF, 4)
+                ish.ishmem_barrier_all()  # everyone's inputs are in place
+                g.launch()
+                hip.stream_synchronize(st_)
+                if int(hip.download(ret, 1, np.int32)[0]) != 0:
+                    fails.append(f"pe{pe} graph replay {rep}: ret != 0")
+                check(f"graph max {rep}", OPS["max"], DT["double"], a, hip.download(d1, n_small, np.float64))
+                check(f"graph sum {rep}", OPS["sum"], DT["float"], b, hip.download(d2, n_big, np.float32))
+                want = np.concatenate([x.view(np.uint8)[:4096] for x in a])
+                if not _bits_equal(hip.download(fc, 4096 * npes, np.uint8), want):
+                    fails.append(f"pe{pe} graph fcollect {rep} wrong")
+                ref = oracle.scan_fold(DT["int32"], [x.view(np.int32) for x in b], pe, True)
+                if not _bits_equal(hip.download(sc, n_big, np.int32), ref):
+                    fails.append(f"pe{pe} graph inscan {rep} wrong")
+            del g
+            hip.stream_destroy(st_)
+            for b_ in (s1, d1, s2, d2, fc, sc, ret):
+                ish.ishmem_free(b_)
 
         if "staged" in scenarios:
             # Host memory and device memory outside the heap go through the staging region.

@@ -83,3 +83,8 @@ def test_launch_parameters_agreed_at_init():
 
 def test_missing_member_times_out_with_error_instead_of_hanging():
     run_pes(2, ["timeout"], timeout=120)
+
+
+@pytest.mark.parametrize("npes", [2, 4])
+def test_hip_graph_capture_and_replay(npes):
+    run_pes(npes, ["graph"])
