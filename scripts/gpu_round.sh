@@ -52,6 +52,11 @@ for s in $STEPS; do
                 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                 --master-port 29541 tools/sweep.py --coll $c --max-mib 256 --min-bytes 4096 --factor 4
             done ;;
+    graph)  for g in "" "--graph"; do
+              ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-128} run graph_p2${g:+_graph} 300 \
+                python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+                --master-port 29551 tools/sweep.py --max-mib 16 --min-bytes 256 --factor 4 --iters 50 $g
+            done ;;
     prof)   cd /tmp && export TMPDIR=/tmp
             run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                 python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline

@@ -24,6 +24,7 @@ def main() -> None:
     ap.add_argument("--min-bytes", type=int, default=4)
     ap.add_argument("--factor", type=int, default=4)
     ap.add_argument("--coll", choices=["reduce", "fcollect", "inscan"], default="reduce")
+    ap.add_argument("--graph", action="store_true", help="time a hipGraph of --iters captured calls")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -47,7 +48,7 @@ def main() -> None:
     hip.upload(src, (np.arange(nmax, dtype=np.int64) % 1024).astype(np.float32) + np.float32(rank))
     st = hip.stream_create()
     if rank == 0:
-        print(f"# coll={args.coll} pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
+        print(f"# coll={args.coll} graph={args.graph} pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
               f"ll_max_bytes={ish.get_param('ll_max_bytes')}")
         print("bytes,us_per_call,algbw_GiBps,ok")
     def call(n):
@@ -74,11 +75,24 @@ def main() -> None:
             dist.barrier()
         e0, e1 = hip.Event(), hip.Event()
         iters = args.iters if n < (1 << 24) else max(3, args.iters // 4)
-        e0.record(st)
-        for _ in range(iters):
-            if call(n):
-                raise RuntimeError(ish.last_error())
-        e1.record(st)
+        if args.graph:
+            with hip.Graph(st) as g:
+                for _ in range(iters):
+                    if call(n):
+                        raise RuntimeError(ish.last_error())
+            g.launch()
+            hip.stream_synchronize(st)
+            if dist is not None:
+                dist.barrier()
+            e0.record(st)
+            g.launch()
+            e1.record(st)
+        else:
+            e0.record(st)
+            for _ in range(iters):
+                if call(n):
+                    raise RuntimeError(ish.last_error())
+            e1.record(st)
         hip.stream_synchronize(st)
         us = e0.elapsed_ms(e1) * 1000.0 / iters
         if dist is not None:
