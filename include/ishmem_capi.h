@@ -176,7 +176,8 @@ void *ishmemi_c_device_ctx(void);
  * "ll_max_bytes" (one-hop granule path threshold, <= 65536), "timeout_ms" (bound on every
  * device-side spin), "stream_order" (1: collectives issued on different streams are ordered by
  * the library in call order, ~2 us per call; 0, the default: the caller orders them, as the
- * reference requires), "debug".  "max_blocks" and "ll_max_bytes" shape every multi-PE launch: init
+ * reference requires), "oneshot_p2_max_bytes" (two-member teams: one-phase fold up to this size,
+ * default 64 MiB), "debug".  "max_blocks" and "ll_max_bytes" shape every multi-PE launch: init
  * agrees on them (minimum over the PEs); a later set_param must be made with the same value on
  * every PE.  ishmemi_c_get_param also reports "staging_bytes" and "flags_fine_grained". */
 const char *ishmemi_c_last_error(void);

@@ -39,6 +39,7 @@ struct ReduceArgs {
     uint64_t tail;    // scalar elements after the body
     uint64_t items_per_chunk;
     uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
+    int oneshot;  // 1: every member folds the WHOLE array (no mid barrier, no all-gather)
     uint32_t *ep_ctr;  // team's kernel-epoch counter: [0] last epoch, [1] workgroups done
     int p, me;
 };

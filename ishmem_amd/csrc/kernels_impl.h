@@ -320,9 +320,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
     // (0, 1, ..., p-1): for compile-time team sizes the p loads are staged in registers and
     // folded by fold_any; at run-time sizes the loop is rotated only where the op is
     // order-insensitive (integers, min, max — bit-identical in any order).
+    const bool one = a.oneshot != 0;
     if (ok) {
-        const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
-        const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
+        const uint64_t cs = one ? 0 : min((uint64_t) me * a.items_per_chunk, a.nitems);
+        const uint64_t ce = one ? a.nitems : min(cs + a.items_per_chunk, a.nitems);
         const int rot = b % p;
         for (uint64_t t0 = cs + (uint64_t) b * kTile; t0 < ce; t0 += G * kTile) {
             if constexpr (P > 0) {
@@ -366,16 +367,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
                 }
             }
         }
-        // Unaligned head (owned by member 0) and tail (owned by member p-1), element-wise.
+        // Unaligned head (owned by member 0) and tail (owned by member p-1; one-shot: both by
+        // every member), element-wise.  Descriptors are based at the region (offsets < 16 B),
+        // never at the array start (a > 2 GiB array would exceed the descriptor's range).
         if (VEC && b == 0) {
             const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
-            // For p >= 2 a member owns at most one of the two regions, so the region base is
-            // wave-uniform; descriptors are based at the region (offsets < 16 B), never at the
-            // array start (a > 2 GiB array would exceed the descriptor's range).
-            const uint64_t rbase = (me == 0 ? 0 : tail_off) * sizeof(T);
-            const bool do_head = (me == 0) && ((uint64_t) tid < a.head);
-            const bool do_tail = (me == p - 1) && ((uint64_t) tid < a.tail);
-            if (do_head || do_tail) {
+            for (int region = 0; region < 2; ++region) {
+                const bool owner = one || (region == 0 ? me == 0 : me == p - 1);
+                const uint64_t cnt = region == 0 ? a.head : a.tail;
+                if (!owner || (uint64_t) tid >= cnt) continue;
+                const uint64_t rbase = (region == 0 ? 0 : tail_off) * sizeof(T);
                 const uint32_t off = (uint32_t) (tid * sizeof(T));
                 T acc = T();
                 for (int j = 0; j < p; ++j) {
@@ -389,10 +390,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
         }
     }
 
-    ok = ok && pe_barrier<true>(a, ep, kPhaseMid, b);
+    if (!one) ok = ok && pe_barrier<true>(a, ep, kPhaseMid, b);
 
     // ---- all-gather: pull every other member's reduced chunk from its dest ----
-    if (ok) {
+    if (ok && !one) {
         for (int k = 0; k < p - 1; ++k) {
             // Peer order rotated by workgroup index: at any instant the workgroups of this PE
             // pull from all p-1 peers at once, i.e. over all p-1 xGMI links, instead of every

@@ -89,7 +89,7 @@ struct PeRecord {
     uint64_t heap_size;
     // Launch-shape parameters: the multi-PE kernels pair workgroup b with workgroup b of every
     // peer and choose the LL path per call, so every PE must use the same values.
-    int64_t max_blocks, ll_max_bytes;
+    int64_t max_blocks, ll_max_bytes, oneshot_p2;
     uint64_t staging_bytes;
     hipIpcMemHandle_t heap_handle;
     hipIpcMemHandle_t flags_handle;
@@ -125,6 +125,10 @@ struct State {
     hipStream_t last_stream = nullptr;
     bool last_stream_set = false;
     bool stream_order = false;
+    // Two-member teams fold the whole array in one phase up to this many bytes
+    // (ISHMEM_ONESHOT_P2_MAX_BYTES; above it the barrier saved is noise and RS + AG's lower HBM
+    // traffic wins where HBM, not the link, bounds).
+    long long oneshot_p2 = 64ll << 20;
     hipEvent_t order_ev = nullptr;
     // Completion of the last use of the staging region (staged pipeline or scan scratch); the
     // next user waits on it, whatever stream it runs on.
@@ -447,6 +451,18 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     a.nitems = pl.nitems;
     a.tail = pl.tail;
     a.items_per_chunk = pl.items_per_chunk;
+    // Two members: reduce-scatter + all-gather moves B over the one link in two halves around a
+    // mid barrier; a one-shot fold of the whole array moves the same B with one barrier less.
+    // Not in place (a member would overwrite its source while the peer still reads it).  The
+    // choice depends only on symmetric-address properties, so every member makes the same one.
+    const uintptr_t d0 = (uintptr_t) dst, s0 = (uintptr_t) src, nb = n * es;
+    if (t.size == 2 && (long long) nb <= s.oneshot_p2 && (d0 + nb <= s0 || s0 + nb <= d0)) {
+        a.oneshot = 1;
+        a.items_per_chunk = pl.nitems;
+        const uint64_t tile = (uint64_t) kBlock * kUnroll;
+        pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((pl.nitems + tile - 1) / tile,
+                                                                   (uint64_t) s.max_blocks));
+    }
     HIP_TRY(launch_allreduce(op, dt, pl.vec, a, pl.grid, st));
     return 0;
 }
@@ -743,6 +759,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
                                          std::max<long long>(0, env_ll("ISHMEM_LL_MAX_BYTES", (long long) kLLDefaultBytes)));
     s.debug = (int) env_ll("ISHMEM_DEBUG", 0);
     s.stream_order = env_ll("ISHMEM_STREAM_ORDER", 0) != 0;
+    s.oneshot_p2 = std::max<long long>(0, env_ll("ISHMEM_ONESHOT_P2_MAX_BYTES", 64ll << 20));
     s.staging_bytes = (parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20) + kHeapAlign - 1) &
                       ~(size_t) (kHeapAlign - 1);
 
@@ -797,6 +814,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.heap_size = s.heap_size;
         mine.max_blocks = s.max_blocks;
         mine.ll_max_bytes = s.ll_max_bytes;
+        mine.oneshot_p2 = s.oneshot_p2;
         mine.staging_bytes = s.staging_bytes;
         HIP_TRY(hipIpcGetMemHandle(&mine.heap_handle, s.heap));
         if (hipIpcGetMemHandle(&mine.flags_handle, s.flags) != hipSuccess) {
@@ -819,6 +837,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         for (int j = 0; j < npes; ++j) {
             s.max_blocks = (int) std::min<int64_t>(s.max_blocks, all[j].max_blocks);
             s.ll_max_bytes = std::min<long long>(s.ll_max_bytes, all[j].ll_max_bytes);
+            s.oneshot_p2 = std::min<long long>(s.oneshot_p2, all[j].oneshot_p2);
             s.staging_bytes = std::min<size_t>(s.staging_bytes, all[j].staging_bytes);
         }
         for (int j = 0; j < npes; ++j) {
@@ -1287,6 +1306,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     if (n == "max_blocks") s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, value));
     else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
     else if (n == "stream_order") s.stream_order = value != 0;
+    else if (n == "oneshot_p2_max_bytes") s.oneshot_p2 = std::max<long long>(0, value);
     else if (n == "ll_max_bytes") s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes, std::max<long long>(0, value));
     else if (n == "debug") s.debug = (int) value;
     else return fail("set_param: unknown parameter " + n);
@@ -1300,6 +1320,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "max_blocks") return s.max_blocks;
     if (n == "timeout_ms") return s.timeout_ms;
     if (n == "stream_order") return s.stream_order ? 1 : 0;
+    if (n == "oneshot_p2_max_bytes") return s.oneshot_p2;
     if (n == "ll_max_bytes") return s.ll_max_bytes;
     if (n == "debug") return s.debug;
     if (n == "flags_fine_grained") return s.flags_fine_grained ? 1 : 0;

@@ -88,3 +88,10 @@ def test_missing_member_times_out_with_error_instead_of_hanging():
 @pytest.mark.parametrize("npes", [2, 4])
 def test_hip_graph_capture_and_replay(npes):
     run_pes(npes, ["graph"])
+
+
+def test_two_pe_reduce_scatter_allgather_path():
+    # At 2 PEs non-in-place reduces take the one-shot fold by default; force the RS + AG kernel
+    # (and no LL) for the same golden / offset / large cases.
+    run_pes(2, ["golden", "offsets", "large"],
+            env={"ISHMEM_ONESHOT_P2_MAX_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_MAX_BLOCKS": 64})
