@@ -111,6 +111,103 @@ def config5_sweep(ish, hip, src, dst, nbytes_max, world, rank, dist, stream):
     return out
 
 
+def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
+    """N>1: the f32 sum again under other launch shapes, set alike on every rank, so the driver's
+    multi-GPU run records how the xGMI path responds (data for choosing the defaults; one
+    MI355X per PE cannot be rehearsed on a one-GPU box):
+      grid  - the payload with the workgroup cap at 128 / 256 / 512 / 1024 (then clamped to the
+              resident capacity);
+      p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
+      ll    - 4 / 16 / 64 KiB with the one-hop granule path on (default) and off."""
+    import torch
+
+    def timed(n, iters):
+        for _ in range(2):
+            ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, stream)
+        hip.stream_synchronize(stream)
+        dist.barrier()
+        e0, e1 = hip.Event(), hip.Event()
+        e0.record(stream)
+        for _ in range(iters):
+            if ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, stream) != 0:
+                raise RuntimeError(ish.last_error())
+        e1.record(stream)
+        hip.stream_synchronize(stream)
+        t = torch.tensor([e0.elapsed_ms(e1) / iters], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    out = []
+
+    def run(case, param, value, nbytes, iters):
+        old = ish.get_param(param)
+        ish.set_param(param, value)
+        try:
+            ms = timed(nbytes // 4, iters)
+        finally:
+            ish.set_param(param, old)
+        out.append({"case": case, param: value, "bytes": nbytes, "us": round(ms * 1e3, 2),
+                    "algbw_GiBps": round(nbytes / GiB / (ms * 1e-3), 2)})
+
+    for mb in (128, 256, 512, 1024):
+        run("grid", "max_blocks", mb, B, 5)
+    if world == 2:
+        run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
+        run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)
+    for nb in (4096, 16384, 65536):
+        run("ll_on", "ll_max_bytes", 65536, nb, 50)
+        run("ll_off", "ll_max_bytes", 0, nb, 50)
+    return out
+
+
+def rccl_allreduce(dist, device, n, B, world, steps, line, limit_s=240.0):
+    """N>1 comparison only: RCCL (torch "nccl" backend) all_reduce of the
+    same f32 payload over the same GPUs, after this library has released its heap.  A watchdog
+    bounds the leg: if RCCL does not finish within limit_s, rank 0 prints the line already
+    measured (marked) and every rank exits, so the main measurement is never lost."""
+    import threading
+
+    import torch
+
+    def expire():
+        if line is not None:
+            line["rccl_allreduce"] = {"error": f"did not finish within {limit_s:.0f} s"}
+            print(json.dumps(line), flush=True)
+        os._exit(0)
+
+    wd = threading.Timer(limit_s, expire)
+    wd.daemon = True
+    wd.start()
+    try:
+        torch.cuda.set_device(device)
+        pg = dist.new_group(backend="nccl")
+        buf = torch.ones(n, dtype=torch.float32, device="cuda")
+        for _ in range(3):
+            dist.all_reduce(buf, group=pg)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            dist.all_reduce(buf, group=pg)
+        torch.cuda.synchronize()
+        tr = time.perf_counter() - t0
+        tt = torch.tensor([tr], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tr = float(tt[0])
+        buf.fill_(1.0)
+        dist.all_reduce(buf, group=pg)
+        ok = bool(torch.all(buf == float(world)).item())
+        del buf
+        torch.cuda.synchronize()
+        dist.destroy_process_group(pg)
+        return {"value": world * B / GiB / (tr / steps), "unit": "GiB/s",
+                "ms_per_step": tr / steps * 1000.0, "steps": steps, "checked": ok}
+    except Exception as ex:
+        return {"error": str(ex)}
+    finally:
+        wd.cancel()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,8 +220,9 @@ def main() -> None:
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--nelems", type=int, default=0, help="override: float32 elements per PE")
-    ap.add_argument("--rccl", action="store_true",
-                    help="N>1: also time RCCL all_reduce on the same payload (comparison only)")
+    ap.add_argument("--no-rccl", action="store_true",
+                    help="N>1: skip the RCCL all_reduce comparison on the same payload")
+    ap.add_argument("--no-tuning", action="store_true", help="N>1: skip the launch-shape sweep")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -311,31 +409,11 @@ def main() -> None:
         except Exception as ex:
             extra["xgmi_probe"] = {"error": str(ex)}
 
-    if world > 1 and (args.rccl or os.environ.get("ISHMEM_BENCH_RCCL") == "1"):
-        # Comparison only: RCCL (torch "nccl" backend) all_reduce of the same payload.
+    if world > 1 and not args.no_tuning:
         try:
-            import torch
-            torch.cuda.set_device(device)
-            pg = dist.new_group(backend="nccl")
-            buf = torch.ones(n, dtype=torch.float32, device="cuda")
-            for _ in range(3):
-                dist.all_reduce(buf, group=pg)
-            torch.cuda.synchronize()
-            dist.barrier()
-            k = args.steps
-            tr0 = time.perf_counter()
-            for _ in range(k):
-                dist.all_reduce(buf, group=pg)
-            torch.cuda.synchronize()
-            tr = time.perf_counter() - tr0
-            tt = torch.tensor([tr], dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            tr = float(tt[0])
-            extra["rccl_allreduce"] = {"value": world * B / GiB / (tr / k), "unit": "GiB/s",
-                                       "ms_per_step": tr / k * 1000.0}
-            del buf
+            extra["xgmi_tuning"] = xgmi_tuning(ish, hip, src, dst, B, world, dist, stream)
         except Exception as ex:
-            extra["rccl_allreduce"] = {"error": str(ex)}
+            extra["xgmi_tuning"] = {"error": str(ex)}
 
     if world > 1 and not args.no_sweep:
         # BASELINE configs[4] (min/max/prod x int32/float64 across the PEs), sizes 4 KiB ..
@@ -363,6 +441,7 @@ def main() -> None:
     ish.ishmem_free(src)
     hip.stream_destroy(stream)
     ish.ishmem_finalize()
+    line = None
     if rank == 0:
         line = {
             "metric": "GiB/s device-resident float32 sum-reduce at 1/2/4/8 PEs vs HBM+xGMI roofline",
@@ -376,7 +455,12 @@ def main() -> None:
             "kernel_ms": kern_ms,
             **({"dev_same_device": True} if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else {}), "roofline": roof, "cpu_baseline": cpu, **extra,
         }
-        print(json.dumps(line))
+    if world > 1 and not args.no_rccl and os.environ.get("ISHMEM_BENCH_SAME_DEVICE") != "1":
+        rccl = rccl_allreduce(dist, device, n, B, world, args.steps, line)
+        if line is not None:
+            line["rccl_allreduce"] = rccl
+    if line is not None:
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

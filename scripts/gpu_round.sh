@@ -29,7 +29,7 @@ nproc > "$OUT/host.txt"; lscpu | grep -m1 "Model name" >> "$OUT/host.txt" || tru
 for s in $STEPS; do
   case "$s" in
     smoke)  run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    gpu)    run pytest_gpu 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    gpu)    run pytest_gpu 1500 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider ;;
     single) run pytest_single 900 python -m pytest tests/test_gpu_single.py -m gpu -x -q -p no:cacheprovider ;;
     multi)  run pytest_multi 1200 python -m pytest tests/test_gpu_multi.py -m gpu -x -q -p no:cacheprovider ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
@@ -39,6 +39,9 @@ for s in $STEPS; do
     local4) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-128} run bench_local4 600 python -m torch.distributed.run \
                 --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 4 \
                 --steps 10 --warmup 3 --mib ${MIB:-512} ;;
+    local8) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-16} ISHMEM_SYMMETRIC_SIZE=1G run bench_local8 600 \
+                python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+                --master-port 29520 bench.py --gpus 8 --steps 5 --warmup 2 --mib ${MIB:-128} ;;
     sweep1) run sweep1 300 python tools/sweep.py --max-mib 1024 ;;
     sweep2) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-256} run sweep2 600 python -m torch.distributed.run \
                 --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 tools/sweep.py --max-mib 256 ;;

@@ -328,8 +328,9 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             ish.ishmem_free(s)
 
         if "large" in scenarios:
-            # f32 sum over 64 Mi elements per PE (256 MiB): full-array comparison.
-            n = 64 << 20
+            # f32 sum over 64 Mi elements per PE (256 MiB; 16 Mi beyond 4 PEs, where every
+            # process holds all p inputs): full-array comparison.
+            n = (64 << 20) if npes <= 4 else (16 << 20)
             s, d = heap(n, DT["float"]), heap(n, DT["float"])
             ins = [oracle.fill_random(DT["float"], 0xABC + j, n) for j in range(npes)]
             hip.upload(s, ins[pe])

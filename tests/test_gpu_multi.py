@@ -90,6 +90,21 @@ def test_hip_graph_capture_and_replay(npes):
     run_pes(npes, ["graph"])
 
 
+@pytest.mark.parametrize("ll", ["on", "off"])
+def test_eight_pes_compile_time_team_size(ll):
+    # p = 8 is the 8 x MI355X node's team size: the register-staged rs_tile<P=8> fold and 8-way
+    # LL rings, with 8 processes on the one GPU (small grids so all eight kernels stay resident).
+    run_pes(8, ["golden", "inplace", "offsets", "edge", "large", "graph"],
+            env={"ISHMEM_MAX_BLOCKS": 8, "ISHMEM_LL_MAX_BYTES": 65536 if ll == "on" else 0},
+            timeout=400)
+
+
+def test_eight_pes_collect_scan_team():
+    # The P=8 scan kernel, 8-member fcollect / collect, strided and 2-D teams of an 8-PE world.
+    run_pes(8, ["collect", "scan", "team"], env={"ISHMEM_MAX_BLOCKS": 8, "ISHMEM_STAGING_SIZE": "4M"},
+            timeout=400)
+
+
 def test_two_pe_reduce_scatter_allgather_path():
     # At 2 PEs non-in-place reduces take the one-shot fold by default; force the RS + AG kernel
     # (and no LL) for the same golden / offset / large cases.
