@@ -21,7 +21,7 @@ constexpr size_t kFlagWordsPerTeam = (size_t) kPhases * kMaxBlocks * kMaxPes;
 constexpr size_t kTeamFlagBytes = kFlagWordsPerTeam * 4 + 256;
 constexpr int kBlock = 256;  // 4 waves of 64
 constexpr int kUnroll = 4;   // items in flight per thread per source (allreduce tiles)
-constexpr int kFaninBlock = 128;  // local combine: one 16-B item per thread, one-shot grid
+constexpr int kFaninBlock = 64;  // local combine: one wave, one 16-B item per thread, one-shot grid
 constexpr int kFaninMaxGrid = 1 << 30;
 
 // Arguments of the multi-PE reduce-scatter + all-gather kernel.  All pointers are already

@@ -438,11 +438,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
 
 // ---------------------------------------------------------------------------------------------
 // Local fan-in combine: dst = op(src_0, ..., src_{k-1}), folded in source order.
-// Measured on MI355X (tools/stream_variants.hip, 1 GiB operands): a one-shot grid with ONE 16-B
-// item per thread and nontemporal loads + stores is the fastest shape (copy 6.59 TB/s = 82 %,
-// a + b 6.57 TB/s = 82 % of the 8 TB/s HBM peak); persistent grid-stride loops with 4-8 items
-// per thread reached only 63-73 %.  NS = 1 / 2 are specialised so every load is in flight
-// before the fold; NS = 0 handles any source count at run time.
+// Measured on MI355X (tools/stream_variants.hip, 1 GiB operands, profiles/r01_extra/
+// stream_variants*.txt): a one-shot grid with ONE 16-B item per thread is the fastest shape;
+// persistent grid-stride loops with 4-8 items per thread reached only 63-73 %, an XCD-aware
+// contiguous block order 77-80 %.  One-wave workgroups with nontemporal loads and
+// system-coherent write-through 16-B stores (sc0 sc1: the line leaves L2 at once, like nt, but
+// the store retires sooner) gave copy 84.2 % / a + b 84.7 % of the 8 TB/s HBM peak, against
+// 81.8 % / 82.2 % for 128-thread blocks with nt stores.  Element-granular (non-vector) items keep
+// nt stores: narrow sc1 stores are one fabric write each (MI355X_MICROARCH.md, store flavours).
+// NS = 1 / 2 are specialised so every load is in flight before the fold; NS = 0 handles any
+// source count at run time.
 // ---------------------------------------------------------------------------------------------
 template <typename I>
 __device__ __forceinline__ I nt_load(const I *p)
@@ -471,7 +476,13 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
             acc = nt_load((const Item *) (a.src[0] + off));
             for (int j = 1; j < a.nsrc; ++j) acc = op1<T, OP>(acc, nt_load((const Item *) (a.src[j] + off)));
         }
-        nt_store((Item *) (a.dst + off), acc);
+        if constexpr (VEC) {
+            // Descriptor based at this workgroup's first item (offsets < 1 KiB, any array size).
+            const char *wbase = uniform_ptr(a.dst + off - (uint64_t) threadIdx.x * IB);
+            wt_store(make_rsrc(wbase), (uint32_t) (threadIdx.x * IB), acc);
+        } else {
+            nt_store((Item *) (a.dst + off), acc);
+        }
     }
     if (VEC && blockIdx.x == 0) {
         const int tid = threadIdx.x;

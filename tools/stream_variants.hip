@@ -91,6 +91,59 @@ __global__ __launch_bounds__(BS) void oneshot(const f4 *__restrict__ a, const f4
     }
 }
 
+// One-shot with an XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs
+// (block b runs on XCD b % 8), so the remap gives each XCD one contiguous eighth of the array.
+template <int NSRC, int BS, bool NTL, bool NTS>
+__global__ __launch_bounds__(BS) void oneshot_xcd(const f4 *__restrict__ a, const f4 *__restrict__ b,
+                                                  f4 *__restrict__ d, long n)
+{
+    const long per = gridDim.x / 8;  // grid is a multiple of 8
+    const long lb = (long) (blockIdx.x % 8) * per + blockIdx.x / 8;
+    const long i = lb * BS + threadIdx.x;
+    if (i < n) {
+        f4 x = ld<NTL>(a + i);
+        if (NSRC == 2) x += ld<NTL>(b + i);
+        st<NTS>(d + i, x);
+    }
+}
+
+// One-shot with system-coherent write-through stores (buffer_store ... sc0 sc1).
+template <int BS>
+__global__ __launch_bounds__(BS) void oneshot_wt(const f4 *__restrict__ a, const f4 *__restrict__ b,
+                                                 f4 *__restrict__ d, long n)
+{
+    const long base = (long) blockIdx.x * BS;
+    const long i = base + threadIdx.x;
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void *) (d + base), (short) 0, 0x7FFFFFFF, 0x00020000);
+    if (i < n) {
+        const f4 x = __builtin_nontemporal_load(a + i);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, x),
+                                               r, threadIdx.x * 16, 0, 17);
+    }
+}
+
+// One-shot with buffer loads / stores and explicit cache-policy bits on both (gfx950 aux:
+// 1 = sc0, 2 = nt, 16 = sc1).
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+template <int NSRC, int BS, int LAUX, int SAUX>
+__global__ __launch_bounds__(BS) void oneshot_aux(const f4 *__restrict__ a, const f4 *__restrict__ b,
+                                                  f4 *__restrict__ d, long n)
+{
+    const long base = (long) blockIdx.x * BS;
+    const __amdgpu_buffer_rsrc_t ra =
+        __builtin_amdgcn_make_buffer_rsrc((void *) (a + base), (short) 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb =
+        __builtin_amdgcn_make_buffer_rsrc((void *) (b + base), (short) 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc((void *) (d + base), (short) 0, 0x7FFFFFFF, 0x00020000);
+    if (base + threadIdx.x < n) {
+        f4 x = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, threadIdx.x * 16, 0, LAUX));
+        if (NSRC == 2) x += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, threadIdx.x * 16, 0, LAUX));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x), rd, threadIdx.x * 16, 0, SAUX);
+    }
+}
+
 // Read-only ceiling: xor-accumulate, one store per thread.
 template <int U, int BS, bool NTL>
 __global__ __launch_bounds__(BS) void readonly(const f4 *__restrict__ a, const f4 *__restrict__ b,
@@ -183,6 +236,26 @@ void LD(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
     hipLaunchKernelGGL((ldsdma_copy<U, BS, NTL, NTS>), dim3(g), dim3(BS), 0, s, a, b, d, n);
 }
 
+template <int NSRC, int BS, bool NTL, bool NTS>
+void OX(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
+{
+    const long g = ((n + BS - 1) / BS + 7) / 8 * 8;
+    hipLaunchKernelGGL((oneshot_xcd<NSRC, BS, NTL, NTS>), dim3(g), dim3(BS), 0, s, a, b, d, n);
+}
+template <int BS>
+void OW(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
+{
+    const long g = (n + BS - 1) / BS;
+    hipLaunchKernelGGL((oneshot_wt<BS>), dim3(g), dim3(BS), 0, s, a, b, d, n);
+}
+
+template <int NSRC, int BS, int LAUX, int SAUX>
+void OA(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
+{
+    const long g = (n + BS - 1) / BS;
+    hipLaunchKernelGGL((oneshot_aux<NSRC, BS, LAUX, SAUX>), dim3(g), dim3(BS), 0, s, a, b, d, n);
+}
+
 void MC(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
 {
     (void) hipMemcpyAsync(d, a, n * 16, hipMemcpyDeviceToDevice, s);
@@ -197,33 +270,81 @@ int main(int argc, char **argv)
     const long bytes = 1l << 30;
     const long n = bytes / 16;
     f4 *a, *b, *d;
-    CK(hipMalloc(&a, bytes));
-    CK(hipMalloc(&b, bytes));
-    CK(hipMalloc(&d, bytes));
+    const std::string layout = argc > 3 ? argv[3] : "separate";
+    if (layout == "separate") {
+        CK(hipMalloc(&a, bytes));
+        CK(hipMalloc(&b, bytes));
+        CK(hipMalloc(&d, bytes));
+    } else {
+        // One heap like the library's symmetric heap: operands at `skew` bytes past 128 MiB and
+        // packed back to back (heap = 256-B aligned first fit after the staging region).
+        const long skew = layout == "heap256" ? 256 : 0;
+        char *h;
+        CK(hipMalloc(&h, 4l << 30));
+        a = (f4 *) (h + (128l << 20) + skew);
+        d = (f4 *) ((char *) a + bytes);
+        b = (f4 *) ((char *) d + bytes);
+    }
     CK(hipMemset(a, 1, bytes));
     CK(hipMemset(b, 2, bytes));
     std::vector<Variant> vs;
-    vs.push_back({"oneshot ns1 U1 bs256 nt/nt", O<1, 1, 256, true, true>, 0, 1});
-    vs.push_back({"oneshot ns1 U1 bs256 nt/plain", O<1, 1, 256, true, false>, 0, 1});
+    const std::string set = argc > 2 ? argv[2] : "all";
+    if (set == "all") {
+        vs.push_back({"oneshot ns1 U1 bs256 nt/nt", O<1, 1, 256, true, true>, 0, 1});
+        vs.push_back({"oneshot ns1 U1 bs256 nt/plain", O<1, 1, 256, true, false>, 0, 1});
+        vs.push_back({"oneshot ns1 U1 bs512 nt/nt", O<1, 1, 512, true, true>, 0, 1});
+        vs.push_back({"oneshot ns1 U1 bs1024 nt/nt", O<1, 1, 1024, true, true>, 0, 1});
+        vs.push_back({"oneshot ns1 U2 bs128 nt/nt", O<1, 2, 128, true, true>, 0, 1});
+        vs.push_back({"oneshot ns1 U4 bs256 nt/nt", O<1, 4, 256, true, true>, 0, 1});
+        vs.push_back({"oneshot ns1 U4 bs64 nt/nt", O<1, 4, 64, true, true>, 0, 1});
+        vs.push_back({"oneshot ns2 U1 bs256 nt/nt", O<2, 1, 256, true, true>, 0, 2});
+        vs.push_back({"oneshot ns2 U1 bs256 nt/plain", O<2, 1, 256, true, false>, 0, 2});
+        vs.push_back({"oneshot ns2 U1 bs512 nt/nt", O<2, 1, 512, true, true>, 0, 2});
+        vs.push_back({"oneshot ns2 U1 bs1024 nt/nt", O<2, 1, 1024, true, true>, 0, 2});
+        vs.push_back({"oneshot ns2 U2 bs128 nt/nt", O<2, 2, 128, true, true>, 0, 2});
+        vs.push_back({"oneshot ns2 U2 bs256 nt/nt", O<2, 2, 256, true, true>, 0, 2});
+        vs.push_back({"writeonly U2 nt bs512 (traffic=1B)", WO<2, 512, true>, 0, 0});
+        vs.push_back({"readonly U2 nt (traffic=1B)", RO<2, 256, true>, 0, 0});
+        vs.push_back({"hipMemcpyAsync D2D", MC, 0, 1});
+    }
+    if (set == "aux") {
+        vs.push_back({"oneshot ns1 U1 bs128 nt/nt", O<1, 1, 128, true, true>, 0, 1});
+        vs.push_back({"aux ns1 bs64  ld nt / st sc0sc1", OA<1, 64, 2, 17>, 0, 1});
+        vs.push_back({"aux ns1 bs128 ld nt / st sc0sc1", OA<1, 128, 2, 17>, 0, 1});
+        vs.push_back({"aux ns1 bs256 ld nt / st sc0sc1", OA<1, 256, 2, 17>, 0, 1});
+        vs.push_back({"aux ns1 bs128 ld nt / st sc1", OA<1, 128, 2, 16>, 0, 1});
+        vs.push_back({"aux ns1 bs128 ld nt / st nt sc1", OA<1, 128, 2, 18>, 0, 1});
+        vs.push_back({"aux ns1 bs128 ld nt / st nt", OA<1, 128, 2, 2>, 0, 1});
+        vs.push_back({"aux ns1 bs128 ld nt / st nt sc0 sc1", OA<1, 128, 2, 19>, 0, 1});
+        vs.push_back({"aux ns1 bs128 ld sc0sc1 / st sc0sc1", OA<1, 128, 17, 17>, 0, 1});
+        vs.push_back({"aux ns1 bs128 ld nt sc0sc1 / st sc0sc1", OA<1, 128, 19, 17>, 0, 1});
+        vs.push_back({"aux ns1 bs64  ld nt / st nt", OA<1, 64, 2, 2>, 0, 1});
+        vs.push_back({"aux ns1 bs64  ld nt / st sc1", OA<1, 64, 2, 16>, 0, 1});
+        vs.push_back({"oneshot ns2 U1 bs128 nt/nt", O<2, 1, 128, true, true>, 0, 2});
+        vs.push_back({"aux ns2 bs64  ld nt / st sc0sc1", OA<2, 64, 2, 17>, 0, 2});
+        vs.push_back({"aux ns2 bs128 ld nt / st sc0sc1", OA<2, 128, 2, 17>, 0, 2});
+        vs.push_back({"aux ns2 bs128 ld nt / st nt", OA<2, 128, 2, 2>, 0, 2});
+        vs.push_back({"aux ns2 bs64  ld nt / st nt", OA<2, 64, 2, 2>, 0, 2});
+        vs.push_back({"aux ns2 bs256 ld nt / st sc0sc1", OA<2, 256, 2, 17>, 0, 2});
+    }
+    // Current product shape (fanin_kernel: one 16-B item per thread, 128-thread blocks) and the
+    // round-1b candidates around it.
+    if (set == "all" || set == "new") {
     vs.push_back({"oneshot ns1 U1 bs128 nt/nt", O<1, 1, 128, true, true>, 0, 1});
-    vs.push_back({"oneshot ns1 U1 bs512 nt/nt", O<1, 1, 512, true, true>, 0, 1});
-    vs.push_back({"oneshot ns1 U1 bs1024 nt/nt", O<1, 1, 1024, true, true>, 0, 1});
-    vs.push_back({"oneshot ns1 U2 bs128 nt/nt", O<1, 2, 128, true, true>, 0, 1});
-    vs.push_back({"oneshot ns1 U4 bs256 nt/nt", O<1, 4, 256, true, true>, 0, 1});
-    vs.push_back({"oneshot ns1 U4 bs64 nt/nt", O<1, 4, 64, true, true>, 0, 1});
-    vs.push_back({"oneshot ns2 U1 bs256 nt/nt", O<2, 1, 256, true, true>, 0, 2});
-    vs.push_back({"oneshot ns2 U1 bs256 nt/plain", O<2, 1, 256, true, false>, 0, 2});
+    vs.push_back({"oneshot ns1 U1 bs64 nt/nt", O<1, 1, 64, true, true>, 0, 1});
+    vs.push_back({"oneshot ns1 U1 bs128 plain/nt", O<1, 1, 128, false, true>, 0, 1});
+    vs.push_back({"oneshot ns1 U1 bs128 plain/plain", O<1, 1, 128, false, false>, 0, 1});
+    vs.push_back({"xcd-remap ns1 bs128 nt/nt", OX<1, 128, true, true>, 0, 1});
+    vs.push_back({"xcd-remap ns1 bs256 nt/nt", OX<1, 256, true, true>, 0, 1});
+    vs.push_back({"wt-store ns1 bs128 nt/sc0sc1", OW<128>, 0, 1});
+    vs.push_back({"lds-dma ns1 U1 bs128 nt/nt", LD<1, 128, true, true>, 0, 1});
+    vs.push_back({"lds-dma ns1 U4 bs256 nt/nt", LD<4, 256, true, true>, 0, 1});
     vs.push_back({"oneshot ns2 U1 bs128 nt/nt", O<2, 1, 128, true, true>, 0, 2});
-    vs.push_back({"oneshot ns2 U1 bs512 nt/nt", O<2, 1, 512, true, true>, 0, 2});
-    vs.push_back({"oneshot ns2 U1 bs1024 nt/nt", O<2, 1, 1024, true, true>, 0, 2});
-    vs.push_back({"oneshot ns2 U2 bs128 nt/nt", O<2, 2, 128, true, true>, 0, 2});
-    vs.push_back({"oneshot ns2 U2 bs256 nt/nt", O<2, 2, 256, true, true>, 0, 2});
+    vs.push_back({"xcd-remap ns2 bs128 nt/nt", OX<2, 128, true, true>, 0, 2});
     vs.push_back({"writeonly U1 plain (traffic=1B)", WO<1, 256, false>, 0, 0});
     vs.push_back({"writeonly U1 nt (traffic=1B)", WO<1, 256, true>, 0, 0});
-    vs.push_back({"writeonly U2 nt bs512 (traffic=1B)", WO<2, 512, true>, 0, 0});
     vs.push_back({"readonly U1 nt (traffic=1B)", RO<1, 256, true>, 0, 0});
-    vs.push_back({"readonly U2 nt (traffic=1B)", RO<2, 256, true>, 0, 0});
-    vs.push_back({"hipMemcpyAsync D2D", MC, 0, 1});
+    }
     hipStream_t s;
     CK(hipStreamCreate(&s));
     hipEvent_t e0, e1;
