@@ -128,6 +128,13 @@ int ishmemi_c_reduce_on_stream(int team, int op, int dtype, void *dest, const vo
  * Device pointers; asynchronous on `stream`. nsrc in 1..16. */
 int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n,
                       void *stream);
+/* Measurement hook (bench.py's xGMI probe, no reference counterpart): dst = sum of the nsrc f32
+ * arrays as 16-B items, every source load issued with the cache policy the collectives would use
+ * on peer memory: policy 0 = nontemporal (L2-cached, nt), 1 = system-coherent (sc0 sc1, what the
+ * reduce / collect / scan kernels issue).  nbytes must be a multiple of 16, pointers 16-B
+ * aligned; srcs may be peers' heap addresses (ishmemi_c_ptr).  Asynchronous on `stream`. */
+int ishmemi_c_pull_probe(void *dst, const void *const *srcs, int nsrc, size_t nbytes, int policy,
+                         void *stream);
 
 /* ---- the collectives next to the reduce, same machinery -------------
  * fcollect: dest[j*nbytes ..] = member j's source, in team order, on every member

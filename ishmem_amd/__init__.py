@@ -191,6 +191,12 @@ def combine(op: str, dtype: str, dst: int, srcs: list[int], n: int, stream: int 
     return _L.ishmemi_c_combine(OPS[op], DTYPES[dtype], dst, arr, len(srcs), n, stream or None)
 
 
+def pull_probe(dst: int, srcs: list[int], nbytes: int, policy: int, stream: int = 0) -> int:
+    """xGMI measurement hook: dst = sum of f32 srcs, loads with cache policy 0 = nt, 1 = sc0 sc1."""
+    arr = (ctypes.c_void_p * len(srcs))(*srcs)
+    return _L.ishmemi_c_pull_probe(dst, arr, len(srcs), nbytes, policy, stream or None)
+
+
 def _make_blocking(op: str, dt: str):
     def fn(*args):
         # Overloads of the reference: (dest, source, nreduce) and (team, dest, source, nreduce).

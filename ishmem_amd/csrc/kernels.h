@@ -22,7 +22,9 @@ constexpr size_t kTeamFlagBytes = kFlagWordsPerTeam * 4 + 256;
 constexpr int kBlock = 256;  // 4 waves of 64
 constexpr int kUnroll = 4;   // items in flight per thread per source (allreduce tiles)
 constexpr int kFaninBlock = 64;  // local combine: one wave, one 16-B item per thread, one-shot grid
-constexpr int kFaninMaxGrid = 1 << 30;
+// AQL grid sizes count work-items in 32 bits: cap the one-shot grid at 2^31 work-items; larger
+// arrays (> 32 GiB of 16-B items) take the kernel's grid-stride loop.
+constexpr int kFaninMaxGrid = (int) ((1ull << 31) / kFaninBlock);
 
 // Arguments of the multi-PE reduce-scatter + all-gather kernel.  All pointers are already
 // translated into this process's address space (own heap or IPC-mapped peer heap).
@@ -114,5 +116,8 @@ hipError_t launch_allreduce(int op, int dt, bool vec, const ReduceArgs &a, int g
                             hipStream_t s);
 hipError_t launch_fanin(int op, int dt, bool vec, const FaninArgs &a, int grid, hipStream_t s);
 hipError_t launch_team_sync(const ReduceArgs &a, hipStream_t s);
+// xGMI measurement hook: dst = sum of a.nsrc f32 arrays (a.nitems 16-B items), source loads with
+// cache policy 0 = nt, 1 = sc0 sc1.
+hipError_t launch_pull_probe(const FaninArgs &a, int policy, hipStream_t s);
 
 }  // namespace ishmemi

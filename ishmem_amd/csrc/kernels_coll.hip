@@ -174,6 +174,32 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
     kernel_epoch_done(a, ep);
 }
 
+// xGMI measurement hook (bench.py xgmi_probe): the same one-wave, one-item-per-thread shape as
+// fanin_kernel, but every source load carries an explicit cache policy so the probe compares
+// the collectives' system-coherent pulls (AUX = sc0 sc1) with nontemporal ones (AUX = nt) over
+// the same links.  All nsrc loads are issued before the sum.
+template <int AUX>
+__global__ __launch_bounds__(kFaninBlock) void pull_probe_kernel(FaninArgs a)
+{
+    using Item = Vec<float>;
+    const uint64_t first = (uint64_t) blockIdx.x * kFaninBlock;
+    const uint32_t off = (uint32_t) (threadIdx.x * sizeof(Item));
+    if (first + threadIdx.x >= a.nitems) return;
+    Item x[kMaxFanin];
+#pragma unroll
+    for (int j = 0; j < kMaxFanin; ++j) {
+        if (j < a.nsrc) {
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(uniform_ptr(a.src[j] + first * sizeof(Item)));
+            x[j] = __builtin_bit_cast(Item, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
+        }
+    }
+    Item acc = x[0];
+#pragma unroll
+    for (int j = 1; j < kMaxFanin; ++j)
+        if (j < a.nsrc) acc = op1<float, ISHMEMI_OP_SUM>(acc, x[j]);
+    wt_store(make_rsrc(uniform_ptr(a.dst + first * sizeof(Item))), off, acc);
+}
+
 template <typename K, typename A>
 hipError_t launch_res(K kernel, const A &a, int grid, hipStream_t s)
 {
@@ -189,6 +215,17 @@ hipError_t launch_collect(const CollectArgs &a, int grid, hipStream_t s)
     if (a.unit == 16) return launch_res(collect_kernel<16>, a, grid, s);
     if (a.unit == 4) return launch_res(collect_kernel<4>, a, grid, s);
     return launch_res(collect_kernel<1>, a, grid, s);
+}
+
+hipError_t launch_pull_probe(const FaninArgs &a, int policy, hipStream_t s)
+{
+    const uint64_t g = (a.nitems + kFaninBlock - 1) / kFaninBlock;
+    if (a.nsrc < 1 || a.nsrc > kMaxFanin || g == 0 || g > (uint64_t) kFaninMaxGrid) return hipErrorInvalidValue;
+    if (policy == 0)
+        hipLaunchKernelGGL(pull_probe_kernel<2>, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(pull_probe_kernel<kSysCoherent>, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a);
+    return hipGetLastError();
 }
 
 template <typename T>

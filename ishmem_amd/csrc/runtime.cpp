@@ -1249,6 +1249,25 @@ int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int
     return 0;
 }
 
+int ishmemi_c_pull_probe(void *dst, const void *const *srcs, int nsrc, size_t nbytes, int policy,
+                         void *stream)
+{
+    if (nsrc < 1 || nsrc > kMaxFanin) return fail("pull_probe: nsrc must be 1..16");
+    if (!dst || !srcs || nbytes % 16 || ((uintptr_t) dst & 15))
+        return fail("pull_probe: 16-B aligned pointers and a multiple of 16 bytes required");
+    if (nbytes == 0) return 0;
+    FaninArgs f{};
+    for (int i = 0; i < nsrc; ++i) {
+        if (!srcs[i] || ((uintptr_t) srcs[i] & 15)) return fail("pull_probe: misaligned or null source");
+        f.src[i] = (const char *) srcs[i];
+    }
+    f.dst = (char *) dst;
+    f.nsrc = nsrc;
+    f.nitems = nbytes / 16;
+    HIP_TRY(launch_pull_probe(f, policy ? 1 : 0, (hipStream_t) stream));
+    return 0;
+}
+
 int ishmemi_c_fcollect(int team, void *dest, const void *source, size_t nbytes)
 {
     return fcollect_impl(team, dest, source, nbytes, nullptr, 0, true);

@@ -75,3 +75,28 @@ def test_device_api_program_builds():
 def test_device_initiated_work_group_reduce(npes):
     """ishmemx_*_reduce_work_group called from a user kernel (include/ishmemx_device.h)."""
     run_exe(build_exe(ROOT / "tests/cpp/device_wg.hip", DEV_EXE), npes)
+
+
+BW_EXE = ROOT / "build" / "reduce_bw"
+
+
+def test_reduce_bw_harness_builds():
+    assert build_exe(ROOT / "tests/cpp/reduce_bw.cpp", BW_EXE).exists()
+
+
+@pytest.mark.gpu
+def test_reduce_bw_harness_runs_and_checks():
+    """The reference's reduce_bw shape (test/performance/reduce_bw.cpp): every mode, result-checked."""
+    key = f"bw{uuid.uuid4().hex[:10]}"
+    exe = build_exe(ROOT / "tests/cpp/reduce_bw.cpp", BW_EXE)
+    procs = []
+    for pe in range(2):
+        env = {**os.environ, "ISHMEM_PE": str(pe), "ISHMEM_NPES": "2", "ISHMEM_DEVICE": "0",
+               "ISHMEM_BOOTSTRAP_KEY": key, "ISHMEM_MAX_BLOCKS": "32", "ISHMEM_TIMEOUT_MS": "20000",
+               "ISHMEM_SYMMETRIC_SIZE": "512M", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+        procs.append(subprocess.Popen([str(exe), "--csv", "-m", "1024"], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs[0][-2000:] + outs[1][-2000:]
+    assert "PASS errors 0" in outs[0]
+    assert outs[0].count("csv,reduce_bw,") >= 4 * 8
