@@ -44,6 +44,32 @@ __global__ void pattern_kernel(const ishmemi_c_device_ctx_t *ctx, int team, T *d
     if (threadIdx.x == 0) *rc = r;
 }
 
+// The reference CTest's "device" mode (test/unit/CMakeLists.txt:35, ishmem_tester.h:1229-1232):
+// the blocking ishmem_<op>_reduce called by ONE work-item inside a kernel.
+template <typename T, int OPC>
+__global__ void device_mode_kernel(const ishmemi_c_device_ctx_t *ctx, T *dest, const T *source, size_t n,
+                                   int *rc)
+{
+    int r;
+    if constexpr (OPC == ISHMEMI_OP_SUM) r = ishmem_sum_reduce(ctx, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_MAX) r = ishmem_max_reduce(ctx, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_MIN) r = ishmem_min_reduce(ctx, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_PROD) r = ishmem_prod_reduce(ctx, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_AND) r = ishmem_and_reduce(ctx, dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_OR) r = ishmem_or_reduce(ctx, dest, source, n);
+    else r = ishmem_xor_reduce(ctx, dest, source, n);
+    *rc = r;
+}
+
+// long_reduce.cpp:145-186: the in-place variant (source == dest) of the produce-then-reduce kernel.
+__global__ void long_reduce_inplace_kernel(const ishmemi_c_device_ctx_t *ctx, long *buf, size_t n, int my_pe,
+                                           int *rc)
+{
+    for (size_t i = threadIdx.x; i < n; i += blockDim.x) buf[i] = (1L << (40 + my_pe)) + (long) i;
+    const int r = ishmemx_long_sum_reduce_work_group(ctx, buf, (const long *) buf, n);
+    if (threadIdx.x == 0) *rc = r;
+}
+
 // sub_group analogue: only the second wavefront of the work-group takes part.
 __global__ void wave_kernel(const ishmemi_c_device_ctx_t *ctx, float *dest, const float *source, size_t n,
                             int *rc)
@@ -82,8 +108,8 @@ static void group_case(const char *what, K kernel, int block, const ishmemi_c_de
 }
 
 template <typename T, int OPC, int ODT>
-static void pattern_case(const ishmemi_c_device_ctx_t *ctx, size_t n, int block, char *sb, char *db,
-                         int *rc)
+static void pattern_case(const ishmemi_c_device_ctx_t *ctx, size_t n, dim3 block, char *sb, char *db,
+                         int *rc, bool single_item = false)
 {
     const int pe = ishmem_my_pe(), npes = ishmem_n_pes();
     const int fam = OPC == OR_AND ? PAT_AND : OPC == OR_OR ? PAT_OR : OPC == OR_XOR ? PAT_XOR : PAT_ARITH;
@@ -92,14 +118,20 @@ static void pattern_case(const ishmemi_c_device_ctx_t *ctx, size_t n, int block,
     oracle_pattern_check(fam, OPC, ODT, npes, n, chk.data());
     (void) hipMemcpy(sb, src.data(), n * sizeof(T), hipMemcpyHostToDevice);
     (void) hipMemset(db, 0, n * sizeof(T));
-    hipLaunchKernelGGL((pattern_kernel<T, OPC>), dim3(1), dim3(block), 0, 0, ctx, ISHMEM_TEAM_WORLD,
-                       (T *) db, (const T *) sb, n, rc);
+    if (single_item)
+        hipLaunchKernelGGL((device_mode_kernel<T, OPC>), dim3(1), dim3(1), 0, 0, ctx, (T *) db, (const T *) sb,
+                           n, rc);
+    else
+        hipLaunchKernelGGL((pattern_kernel<T, OPC>), dim3(1), block, 0, 0, ctx, ISHMEM_TEAM_WORLD,
+                           (T *) db, (const T *) sb, n, rc);
     (void) hipDeviceSynchronize();
     int r = -1;
     (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);
     (void) hipMemcpy(got.data(), db, n * sizeof(T), hipMemcpyDeviceToHost);
     if (r != 0 || memcmp(got.data(), chk.data(), n * sizeof(T)) != 0) {
-        if (++errors <= 16) printf("[%d] FAIL device pattern op %d dt %d n %zu rc %d\n", pe, OPC, ODT, n, r);
+        if (++errors <= 16)
+            printf("[%d] FAIL device pattern op %d dt %d n %zu block %ux%ux%u single %d rc %d\n", pe, OPC, ODT, n,
+                   block.x, block.y, block.z, (int) single_item, r);
     }
 }
 
@@ -143,6 +175,40 @@ int main()
         pattern_case<uint64_t, OR_XOR, OD_UINT64>(ctx, n, 512, sb, db, rc);
         pattern_case<uint8_t, OR_AND, OD_UINT8>(ctx, n, 256, sb, db, rc);
         pattern_case<uint32_t, OR_OR, OD_UINT32>(ctx, n, 256, sb, db, rc);
+    }
+    // In place (long_reduce.cpp:145-186).
+    for (size_t n : {1, 100, 4096, 65536}) {
+        hipLaunchKernelGGL(long_reduce_inplace_kernel, dim3(1), dim3(256), 0, 0, ctx, (long *) sb, n, pe, rc);
+        (void) hipDeviceSynchronize();
+        std::vector<long> got(n);
+        int r = -1;
+        (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);
+        (void) hipMemcpy(got.data(), sb, n * sizeof(long), hipMemcpyDeviceToHost);
+        const long mask = ((1L << npes) - 1) << 40;
+        size_t bad = 0;
+        for (size_t i = 0; i < n; ++i) bad += got[i] != mask + (long) i * npes;
+        if (r != 0 || bad) {
+            if (++errors <= 16) printf("[%d] FAIL long_reduce in place n %zu rc %d bad %zu\n", pe, n, r, bad);
+        }
+    }
+    // "device" mode (one work-item) over every valid (op, dtype) with the testers' patterns.
+    for (size_t n : {1, 17, 129}) {
+#define DM(T, OPC, ODT) pattern_case<T, OPC, ODT>(ctx, n, dim3(1), sb, db, rc, true);
+#define DM_INT(OPC) DM(int8_t, OPC, OD_INT8) DM(int16_t, OPC, OD_INT16) DM(int32_t, OPC, OD_INT32) \
+    DM(int64_t, OPC, OD_INT64) DM(uint8_t, OPC, OD_UINT8) DM(uint16_t, OPC, OD_UINT16) DM(uint32_t, OPC, OD_UINT32) \
+    DM(uint64_t, OPC, OD_UINT64)
+#define DM_ALL(OPC) DM_INT(OPC) DM(float, OPC, OD_FLOAT) DM(double, OPC, OD_DOUBLE)
+        DM_INT(OR_AND) DM_INT(OR_OR) DM_INT(OR_XOR)
+        DM_ALL(OR_MAX) DM_ALL(OR_MIN) DM_ALL(OR_SUM) DM_ALL(OR_PROD)
+#undef DM_ALL
+#undef DM_INT
+#undef DM
+    }
+    // device_grp2 / device_grp3: 2-D and 3-D work-groups (team_reduce_test.h TEST_GRP2_FN / GRP3).
+    for (size_t n : {1, 1000, 4097}) {
+        pattern_case<float, OR_SUM, OD_FLOAT>(ctx, n, dim3(16, 16), sb, db, rc);
+        pattern_case<int64_t, OR_MAX, OD_INT64>(ctx, n, dim3(8, 4, 8), sb, db, rc);
+        pattern_case<uint16_t, OR_XOR, OD_UINT16>(ctx, n, dim3(32, 2, 2), sb, db, rc);
     }
     for (size_t n : {1, 63, 64, 1000, 20000}) {
         group_case<decltype(&wave_kernel), float, OR_SUM, OD_FLOAT>("wavefront float sum", wave_kernel, 256, ctx,
