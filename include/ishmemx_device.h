@@ -84,6 +84,50 @@ __device__ __forceinline__ char *peer_addr(const ishmemi_c_device_ctx_t *c, cons
     return c->peer_heap[pe] + ((const char *) p - c->heap_base);
 }
 
+// 16 bytes of T, the unit of the vectorised fold.
+template <typename T>
+struct alignas(16) Vec16 {
+    T e[16 / sizeof(T)];
+};
+constexpr int kUnroll = 4;  // 16-B items in flight per thread and member
+
+template <typename T, int OP>
+__device__ __forceinline__ Vec16<T> op16(const Vec16<T> &a, const Vec16<T> &b)
+{
+    Vec16<T> r;
+#pragma unroll
+    for (int i = 0; i < (int) (16 / sizeof(T)); ++i) r.e[i] = op1<T, OP>(a.e[i], b.e[i]);
+    return r;
+}
+
+// A pointer every calling thread holds with the same value, moved to scalar registers (buffer
+// descriptors need a uniform base; the group's threads all compute the same address).
+__device__ __forceinline__ const char *group_uniform(const char *p)
+{
+    const uint64_t v = (uint64_t) p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t) v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t) (v >> 32));
+    return (const char *) (((uint64_t) hi << 32) | lo);
+}
+
+// System-coherent (sc0 sc1) 16-B load / write-through store through a buffer descriptor based at
+// `base`; off < 2 GiB.
+template <typename T>
+__device__ __forceinline__ Vec16<T> sys_load16(const char *base, uint32_t off)
+{
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), (short) 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_bit_cast(Vec16<T>, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 17));
+}
+
+template <typename T>
+__device__ __forceinline__ void sys_store16(char *base, uint32_t off, const Vec16<T> &v)
+{
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short) 0, 0x7FFFFFFF, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 17);
+}
+
 // Execution groups that can call a device collective (the reference's `const Group &grp`:
 // sycl::group<1..3> and sycl::sub_group, plus the single work-item of a device-side blocking
 // call).  Every member of the group calls with identical arguments.
@@ -179,7 +223,35 @@ __device__ int reduce_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, 
     const size_t cs = (size_t) me * per < nreduce ? (size_t) me * per : nreduce;
     const size_t ce = cs + per < nreduce ? cs + per : nreduce;
     const int start = c->team_start[team], stride = c->team_stride[team];
-    for (size_t i = cs + tid; i < ce; i += nthr) {
+    // 16-B items when both arrays are 16-B aligned (chunk edges are multiples of 64 elements, and
+    // every heap is mapped at the same offsets, so peers' addresses share the residue); the few
+    // elements of the last chunk past its last whole item, and misaligned arrays, go element-wise.
+    constexpr size_t E = 16 / sizeof(T);
+    const bool vec = ((((uintptr_t) dest) | ((uintptr_t) source)) & 15) == 0;
+    const size_t nv = vec ? (ce - cs) / E : 0;
+    for (size_t v0 = 0; v0 < nv; v0 += (size_t) nthr * kUnroll) {
+        Vec16<T> acc[kUnroll];
+        for (int j = 0; j < size; ++j) {
+            const int gpe = start + j * stride;
+            const char *base = (j == me) ? (const char *) (source + cs) : peer_addr(c, source + cs, gpe);
+            const char *step = group_uniform(base + v0 * 16);
+            Vec16<T> x[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const size_t k = (size_t) u * nthr + tid;
+                if (v0 + k < nv) x[u] = sys_load16<T>(step, (uint32_t) (k * 16));
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) acc[u] = (j == 0) ? x[u] : op16<T, OP>(acc[u], x[u]);
+        }
+        char *dstep = (char *) group_uniform((const char *) (dest + cs) + v0 * 16);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const size_t k = (size_t) u * nthr + tid;
+            if (v0 + k < nv) sys_store16<T>(dstep, (uint32_t) (k * 16), acc[u]);  // write-through
+        }
+    }
+    for (size_t i = cs + nv * E + tid; i < ce; i += nthr) {
         T acc = T();
         for (int j = 0; j < size; ++j) {
             const int gpe = start + j * stride;
@@ -194,7 +266,25 @@ __device__ int reduce_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, 
         const int gpe = start + j * stride;
         const size_t js = (size_t) j * per < nreduce ? (size_t) j * per : nreduce;
         const size_t je = js + per < nreduce ? js + per : nreduce;
-        for (size_t i = js + tid; i < je; i += nthr) dest[i] = sys_load((const T *) peer_addr(c, dest + i, gpe));
+        const size_t jv = vec ? (je - js) / E : 0;
+        const char *pbase = peer_addr(c, dest + js, gpe);
+        for (size_t v0 = 0; v0 < jv; v0 += (size_t) nthr * kUnroll) {
+            const char *step = group_uniform(pbase + v0 * 16);
+            Vec16<T> x[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const size_t q = (size_t) u * nthr + tid;
+                if (v0 + q < jv) x[u] = sys_load16<T>(step, (uint32_t) (q * 16));
+            }
+            Vec16<T> *dp = (Vec16<T> *) (dest + js) + v0;
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const size_t q = (size_t) u * nthr + tid;
+                if (v0 + q < jv) dp[q] = x[u];
+            }
+        }
+        for (size_t i = js + jv * E + tid; i < je; i += nthr)
+            dest[i] = sys_load((const T *) peer_addr(c, dest + i, gpe));
     }
     // End: no member returns while a peer may still read its dest.
     return group_barrier<G>(c, team, 2, epoch, false) ? 0 : 1;
