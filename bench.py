@@ -31,6 +31,9 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# Bound every device-side spin to 15 s (library default 60 s): a PE that never arrives ends the
+# run with an error line within a minute instead of stalling every queued step for a minute each.
+os.environ.setdefault("ISHMEM_TIMEOUT_MS", "15000")
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 XGMI_LINK_GBS = 153.6       # per link, as given by the task brief (may be bidirectional)
@@ -271,6 +274,8 @@ def main() -> None:
     for _ in range(args.warmup):
         step()
     barrier()
+    if ish.lib().ishmemi_c_error_count():
+        raise RuntimeError("device barrier timeouts during warm-up (a PE did not arrive)")
     ev0, ev1 = hip.Event(), hip.Event()
     t0 = time.perf_counter()
     ev0.record(stream)
