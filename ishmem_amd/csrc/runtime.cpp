@@ -1354,9 +1354,14 @@ long long ishmemi_c_get_param(const char *name)
 
 int ishmemi_c_error_count(void)
 {
+    // Errors already reported by blocking calls, plus error words the device has set since and no
+    // blocking call has collected yet (stream-ordered collectives and the device API).
     State &s = S();
-    const int dev = (s.err_host && s.err_host[kMaxTeams]) ? 1 : 0;
-    return s.error_count + dev;
+    int pending = 0;
+    if (s.err_host)
+        for (int t = 0; t <= kMaxTeams; ++t)
+            pending += __atomic_load_n(&s.err_host[t], __ATOMIC_ACQUIRE) != 0;
+    return s.error_count + pending;
 }
 
 size_t ishmemi_c_dtype_size(int dtype)
