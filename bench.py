@@ -152,8 +152,12 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
         out.append({"case": case, param: value, "bytes": nbytes, "us": round(ms * 1e3, 2),
                     "algbw_GiBps": round(nbytes / GiB / (ms * 1e-3), 2)})
 
+    # Several PEs sharing one GPU (ISHMEM_BENCH_SAME_DEVICE rehearsals) must keep their summed
+    # grids resident, so there the sweep stays at or below the grid cap the run started with.
+    cap = ish.get_param("max_blocks") if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else 1024
     for mb in (128, 256, 512, 1024):
-        run("grid", "max_blocks", mb, B, 5)
+        if mb <= cap:
+            run("grid", "max_blocks", mb, B, 5)
     if world == 2:
         run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
         run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)
@@ -209,6 +213,12 @@ def rccl_allreduce(dist, device, n, B, world, steps, line, limit_s=240.0):
         return {"error": str(ex)}
     finally:
         wd.cancel()
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (rank 0), so a long leg is visibly alive; stdout keeps the one JSON line."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def main() -> None:
@@ -271,6 +281,7 @@ def main() -> None:
         if r != 0:
             raise RuntimeError(f"reduce failed: {ish.last_error()}")
 
+    log("warm-up")
     for _ in range(args.warmup):
         step()
     barrier()
@@ -318,6 +329,7 @@ def main() -> None:
     roof["frac"] = roof["achieved"] / roof["peak"]
 
     extra = {}
+    log("timed steps done; combine leg")
     if world == 1 and not args.no_combine:
         # Local combine unit dst = a + b at the same size (3B HBM bytes per launch).
         b2 = ish.ishmem_malloc(B)
@@ -337,6 +349,7 @@ def main() -> None:
                             "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("combine2_1pe", B)}
         ish.ishmem_free(b2)
 
+    log("host-memory end-to-end leg")
     if not args.no_e2e:
         # The path starts and ends in host memory (north star): pinned host source/dest, the
         # library stages H2D -> device reduce -> D2H through HBM as a 3-stream pipeline.
@@ -372,6 +385,7 @@ def main() -> None:
         except Exception as ex:  # reported, never fatal for the main measurement
             extra["e2e_host"] = {"error": str(ex)}
 
+    log("xGMI probe")
     if world > 1 and not args.no_probe:
         # Measured link rates (report against the spec AND a measured L).  Plain
         # pulls of a peer's source through the local combine kernel, no barriers inside:
@@ -425,18 +439,21 @@ def main() -> None:
         except Exception as ex:
             extra["xgmi_probe"] = {"error": str(ex)}
 
+    log("launch-shape sweep")
     if world > 1 and not args.no_tuning:
         try:
             extra["xgmi_tuning"] = xgmi_tuning(ish, hip, src, dst, B, world, dist, stream)
         except Exception as ex:
             extra["xgmi_tuning"] = {"error": str(ex)}
 
+    log("config-5 sweep")
     if world > 1 and not args.no_sweep:
         # BASELINE configs[4] (min/max/prod x int32/float64 across the PEs), sizes 4 KiB ..
         # the payload (1 GiB) per PE (the 4 GiB end of that sweep is left to tools/sweep.py).  Inputs
         # x_pe[i] = (i mod 1024) + pe; every result is checked against the canonical fold.
         extra["config5_sweep"] = config5_sweep(ish, hip, src, dst, B, world, rank, dist, stream)
 
+    log("CPU baseline leg")
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         import oracle  # CPU baseline leg only: the reference's host-proxy reduce, restated
@@ -472,6 +489,7 @@ def main() -> None:
             **({"dev_same_device": True} if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else {}), "roofline": roof, "cpu_baseline": cpu, **extra,
         }
     if world > 1 and not args.no_rccl and os.environ.get("ISHMEM_BENCH_SAME_DEVICE") != "1":
+        log("RCCL comparison leg")
         rccl = rccl_allreduce(dist, device, n, B, world, args.steps, line)
         if line is not None:
             line["rccl_allreduce"] = rccl
