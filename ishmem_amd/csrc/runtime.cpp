@@ -864,8 +864,43 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             }
             HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_heap[j], all[j].heap_handle,
                                         hipIpcMemLazyEnablePeerAccess));
-            HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_flags[j], all[j].flags_handle,
-                                        hipIpcMemLazyEnablePeerAccess));
+        }
+        // Flags (+ LL rings): if any PE cannot import a peer's fine-grained export, every PE
+        // re-exports a coarse-grained block instead (every flag and granule access is a
+        // system-scope atomic, so the protocol does not depend on the memory type).
+        int32_t opened = 1;
+        for (int j = 0; j < npes && opened; ++j) {
+            if (j == pe) continue;
+            if (hipIpcOpenMemHandle((void **) &s.peer_flags[j], all[j].flags_handle,
+                                    hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                (void) hipGetLastError();
+                s.peer_flags[j] = nullptr;
+                opened = 0;
+            }
+        }
+        int32_t all_opened[kMaxPes];
+        if (s.boot.allgather(&opened, all_opened, sizeof(int32_t), err)) return fail(err);
+        bool retry = false;
+        for (int j = 0; j < npes; ++j) retry = retry || !all_opened[j];
+        if (retry) {
+            for (int j = 0; j < npes; ++j) {
+                if (j != pe && s.peer_flags[j]) (void) hipIpcCloseMemHandle(s.peer_flags[j]);
+                s.peer_flags[j] = nullptr;
+            }
+            if (s.boot.barrier(err)) return fail(err);  // no peer still maps our old block
+            (void) hipFree(s.flags);
+            HIP_TRY(hipMalloc((void **) &s.flags, flag_bytes));
+            HIP_TRY(hipMemset(s.flags, 0, flag_bytes));
+            HIP_TRY(hipDeviceSynchronize());
+            s.flags_fine_grained = false;
+            s.peer_flags[pe] = s.flags;
+            hipIpcMemHandle_t h, hs[kMaxPes];
+            HIP_TRY(hipIpcGetMemHandle(&h, s.flags));
+            if (s.boot.allgather(&h, hs, sizeof(h), err)) return fail(err);
+            for (int j = 0; j < npes; ++j) {
+                if (j == pe) continue;
+                HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_flags[j], hs[j], hipIpcMemLazyEnablePeerAccess));
+            }
         }
         if (s.boot.barrier(err)) return fail(err);
     }
