@@ -116,8 +116,9 @@ int ishmemi_c_team_sync(int team);
  * ishmemi_c_reduce_on_stream: the HIP-stream analogue of
  *   sycl::event ishmemx_<TYPENAME>_<op>_reduce_on_queue(..., int *ret, sycl::queue &q, deps)
  * (src/ishmemx.h:1172-1803, src/collectives/reduce_impl.h:444-474): enqueues the collective on
- * `stream` (hipStream_t) and returns at once; the kernel writes 0 to *ret (device-visible int,
- * may be NULL) on success (reduce_impl.h:461-463). */
+ * `stream` (hipStream_t) and returns at once.  *ret (device-visible int, may be NULL) is set to 0
+ * in stream order at the start of the call and to nonzero by any of the call's launches that
+ * fails, so it reads 0 after the call completes only on success (reduce_impl.h:461-463). */
 int ishmemi_c_reduce(int team, int op, int dtype, void *dest, const void *source, size_t nreduce);
 int ishmemi_c_reduce_on_stream(int team, int op, int dtype, void *dest, const void *source,
                                size_t nreduce, int *ret, void *stream);
@@ -135,6 +136,10 @@ int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int
  * aligned; srcs may be peers' heap addresses (ishmemi_c_ptr).  Asynchronous on `stream`. */
 int ishmemi_c_pull_probe(void *dst, const void *const *srcs, int nsrc, size_t nbytes, int policy,
                          void *stream);
+/* Test hook (no reference counterpart): enqueues on `stream` a kernel of `grid` workgroups that
+ * each hold half a CU (1024 work-items, 80 KiB of LDS) for `usec` microseconds (<= 60 s), so a
+ * test can run collectives while another kernel holds most CUs. */
+int ishmemi_c_occupy(int grid, unsigned long long usec, void *stream);
 
 /* ---- the collectives next to the reduce, same machinery -------------
  * fcollect: dest[j*nbytes ..] = member j's source, in team order, on every member
@@ -184,9 +189,11 @@ void *ishmemi_c_device_ctx(void);
  * device-side spin), "stream_order" (1: collectives issued on different streams are ordered by
  * the library in call order, ~2 us per call; 0, the default: the caller orders them, as the
  * reference requires), "oneshot_p2_max_bytes" (two-member teams: one-phase fold up to this size,
- * default 64 MiB), "debug".  "max_blocks" and "ll_max_bytes" shape every multi-PE launch: init
- * agrees on them (minimum over the PEs); a later set_param must be made with the same value on
- * every PE.  ishmemi_c_get_param also reports "staging_bytes" and "flags_fine_grained". */
+ * default 64 MiB), "debug".  "ll_max_bytes" and "oneshot_p2_max_bytes" choose the kernel of a
+ * multi-PE call: init agrees on them (minimum over the PEs) and a later set_param must be made
+ * with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,
+ * nothing is paired by workgroup index).  ishmemi_c_get_param also reports "staging_bytes",
+ * "heap_bytes", "flags_fine_grained" and "cu_count" (compute units of this PE's device). */
 const char *ishmemi_c_last_error(void);
 int ishmemi_c_set_param(const char *name, long long value);
 long long ishmemi_c_get_param(const char *name);

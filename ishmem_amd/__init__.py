@@ -168,6 +168,14 @@ def set_param(name: str, value: int) -> int:
     return _L.ishmemi_c_set_param(name.encode(), int(value))
 
 
+def chunk_bounds(nitems: int, npes: int, c: int) -> tuple[int, int]:
+    """Member c's [begin, end) of the multi-PE partition of `nitems` 16-B items (test hook)."""
+    b, e = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    if _L.ishmemi_c_chunk_bounds(nitems, npes, c, ctypes.byref(b), ctypes.byref(e)):
+        raise ValueError("chunk_bounds: invalid arguments")
+    return b.value, e.value
+
+
 def get_param(name: str) -> int:
     return int(_L.ishmemi_c_get_param(name.encode()))
 
@@ -195,6 +203,11 @@ def pull_probe(dst: int, srcs: list[int], nbytes: int, policy: int, stream: int 
     """xGMI measurement hook: dst = sum of f32 srcs, loads with cache policy 0 = nt, 1 = sc0 sc1."""
     arr = (ctypes.c_void_p * len(srcs))(*srcs)
     return _L.ishmemi_c_pull_probe(dst, arr, len(srcs), nbytes, policy, stream or None)
+
+
+def occupy(grid: int, usec: int, stream: int = 0) -> int:
+    """Test hook: `grid` workgroups that each hold half a CU for `usec` microseconds."""
+    return _L.ishmemi_c_occupy(grid, usec, stream or None)
 
 
 def _make_blocking(op: str, dt: str):

@@ -63,8 +63,32 @@ int ShmBootstrap::attach(int pe, int npes, const std::string &key, int timeout_m
     bytes_ = sizeof(Header) + (size_t) npes * kSlotBytes;
     const double t0 = now_ms();
     if (pe == 0) {
-        shm_unlink(name_.c_str());  // a stale segment of a crashed run
         int fd = shm_open(name_.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0 && errno == EEXIST) {
+            // A segment of this name exists: a crashed run's (its creator is gone: remove it) or
+            // a live job's (refuse, instead of silently joining or unlinking another job).
+            int32_t owner = 0;
+            int efd = shm_open(name_.c_str(), O_RDONLY, 0600);
+            if (efd >= 0) {
+                struct stat st;
+                if (fstat(efd, &st) == 0 && (size_t) st.st_size >= sizeof(Header)) {
+                    void *b = mmap(nullptr, sizeof(Header), PROT_READ, MAP_SHARED, efd, 0);
+                    if (b != MAP_FAILED) {
+                        const Header *h = reinterpret_cast<const Header *>(b);
+                        if (h->magic.load(std::memory_order_acquire) == kMagic) owner = h->creator_pid;
+                        munmap(b, sizeof(Header));
+                    }
+                }
+                close(efd);
+            }
+            if (owner > 0 && owner != (int32_t) getpid() && (kill(owner, 0) == 0 || errno == EPERM)) {
+                err = "bootstrap: key '" + key + "' is in use by a live job (pid " +
+                      std::to_string(owner) + "); set ISHMEM_BOOTSTRAP_KEY to a unique value";
+                return 1;
+            }
+            shm_unlink(name_.c_str());
+            fd = shm_open(name_.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+        }
         if (fd < 0) {
             err = "bootstrap: shm_open(create) failed: " + std::string(strerror(errno));
             return 1;

@@ -13,10 +13,18 @@ namespace ishmemi {
 constexpr int kMaxPes = 16;
 // Upper bound of workgroups per collective launch; flag arrays are sized from it.
 constexpr int kMaxBlocks = 1024;
-// Barrier phases of one collective (start, mid, end) + a standalone team-sync phase.
+// Flag rows of one team, [phase][slot][pe] u32 epochs written by peers into this PE's block:
+//   kPhaseStart, slot 0 - member pe's launch has started (its source is final);
+//   kPhaseMid, slot s   - member pe's reduced segment s (or, for a scan, all of its chunk) is
+//                         stored and readable;
+//   kPhaseEnd, slot 0   - member pe has finished every read of this PE's memory;
+//   kPhaseSync, slot 0  - standalone team barrier.
+// A launch never pairs its workgroups with a peer's: any workgroup may satisfy a start flag,
+// segments are grabbed from a per-launch work counter, and only the launch's last workgroup
+// waits for the peers' end flags, so progress never depends on which workgroups are resident.
 constexpr int kPhases = 4;
 constexpr int kPhaseStart = 0, kPhaseMid = 1, kPhaseEnd = 2, kPhaseSync = 3;
-// Per-team flag block: [phase][block][pe] uint32 epochs, then an error word.
+// Per-team flag block: [phase][slot][pe] uint32 epochs, then an error word.
 constexpr size_t kFlagWordsPerTeam = (size_t) kPhases * kMaxBlocks * kMaxPes;
 constexpr size_t kTeamFlagBytes = kFlagWordsPerTeam * 4 + 256;
 constexpr int kBlock = 256;  // 4 waves of 64
@@ -26,6 +34,17 @@ constexpr int kFaninBlock = 64;  // local combine: one wave, one 16-B item per t
 // arrays (> 32 GiB of 16-B items) take the kernel's grid-stride loop.
 constexpr int kFaninMaxGrid = (int) ((1ull << 31) / kFaninBlock);
 
+// Per-team launch words (device memory, uncached, kEpWords u32 per team; `ep_ctr` in the
+// argument structs points at the team's first word).  All are zero between launches except
+// kEpEpoch; the launch's last workgroup resets the others.
+constexpr int kEpWords = 16;
+constexpr int kEpEpoch = 0;    // epoch of the team's last launch
+constexpr int kEpDone = 1;     // workgroups of this launch that have finished
+constexpr int kEpRsHead = 2;   // next reduce-scatter segment (scan: phase-1 piece) to grab
+constexpr int kEpAgHead = 3;   // next all-gather item to grab
+constexpr int kEpStarted = 4;  // workgroups that have started (the first announces the launch)
+constexpr int kEpFail = 5;     // nonzero once any wait of this launch timed out: drain at once
+constexpr int kEpP1Done = 6;   // scan: phase-1 pieces completed
 // Arguments of the multi-PE reduce-scatter + all-gather kernel.  All pointers are already
 // translated into this process's address space (own heap or IPC-mapped peer heap).
 struct ReduceArgs {
@@ -40,9 +59,10 @@ struct ReduceArgs {
     uint64_t nitems;  // body items (16-B vectors in vector mode, elements in scalar mode)
     uint64_t tail;    // scalar elements after the body
     uint64_t items_per_chunk;
+    uint64_t seg_items;      // items per reduce-scatter segment (a multiple of kBlock*kUnroll)
     uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
-    int oneshot;  // 1: every member folds the WHOLE array (no mid barrier, no all-gather)
-    uint32_t *ep_ctr;  // team's kernel-epoch counter: [0] last epoch, [1] workgroups done
+    int oneshot;  // 1: every member folds the WHOLE array (no hand-off, no all-gather)
+    uint32_t *ep_ctr;  // team's launch words (kEpWords, see kEp*)
     int p, me;
 };
 
@@ -61,13 +81,13 @@ struct LLArgs {
     int *ret;
     uint64_t nbytes;
     uint64_t timeout_ticks;
-    uint32_t *ep_ctr;  // team's kernel-epoch counter: [0] last epoch, [1] workgroups done
+    uint32_t *ep_ctr;  // team's launch words (kEpWords, see kEp*)
     int p, me;
 };
 hipError_t launch_ll(int op, int dt, const LLArgs &a, hipStream_t s);
 
 // fcollect / collect (all-gather of the members' sources): member j's bytes land at
-// dst + dst_off[j].  Same pairwise barriers as the reduce (start, end).
+// dst + dst_off[j].  Same start / finish protocol as the reduce.
 struct CollectArgs {
     const char *src[kMaxPes];  // member j's source, mapped here
     char *dst;
@@ -78,7 +98,7 @@ struct CollectArgs {
     uint32_t *err;
     int *ret;
     uint64_t timeout_ticks;
-    uint32_t *ep_ctr;  // team's kernel-epoch counter: [0] last epoch, [1] workgroups done
+    uint32_t *ep_ctr;  // team's launch words (kEpWords, see kEp*)
     int p, me;
     int unit;  // bytes per item: 16, 4 or 1 (largest dividing every address and length)
 };
@@ -95,7 +115,7 @@ struct ScanArgs {
     int *ret;
     uint64_t nelems, items_per_chunk;
     uint64_t timeout_ticks;
-    uint32_t *ep_ctr;  // team's kernel-epoch counter: [0] last epoch, [1] workgroups done
+    uint32_t *ep_ctr;  // team's launch words (kEpWords, see kEp*)
     int p, me;
     int inclusive;
 };
@@ -119,5 +139,13 @@ hipError_t launch_team_sync(const ReduceArgs &a, hipStream_t s);
 // xGMI measurement hook: dst = sum of a.nsrc f32 arrays (a.nitems 16-B items), source loads with
 // cache policy 0 = nt, 1 = sc0 sc1.
 hipError_t launch_pull_probe(const FaninArgs &a, int policy, hipStream_t s);
+// PEs that share this process's GPU (several PEs per device: tests and rehearsals).  Each
+// multi-PE launch then takes at most 1/share of the device's resident workgroups, so every
+// co-located PE's launch fits at once and one PE's waiting workgroups can never hold the CUs a
+// co-located peer needs to make progress (across GPUs that cannot happen).
+void set_device_share(int share);
+int device_share();
+// Test hook: `grid` workgroups that each hold half a CU (1024 work-items, 80 KiB LDS) for `usec`.
+hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s);
 
 }  // namespace ishmemi

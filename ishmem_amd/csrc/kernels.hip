@@ -4,6 +4,12 @@
 
 namespace ishmemi {
 
+namespace {
+int g_device_share = 1;
+}
+void set_device_share(int share) { g_device_share = share < 1 ? 1 : share; }
+int device_share() { return g_device_share; }
+
 #define ISHMEMI_DECL_OP(N)                                                                         \
     hipError_t launch_allreduce_op##N(int dt, bool vec, const ReduceArgs &a, int grid,             \
                                       hipStream_t s);                                              \

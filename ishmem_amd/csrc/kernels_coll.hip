@@ -13,7 +13,8 @@ namespace ishmemi {
 namespace {
 
 // All-gather of the sources: workgroup b copies tiles t == b (mod G) of every member's source,
-// member order rotated by workgroup (all links busy), local slot included.  Only remote LOADS.
+// member order rotated by workgroup (all links busy), local slot included.  Only remote LOADS;
+// between launch_start and launch_finish nothing waits, so the static tile split is safe.
 template <int U>
 __global__ __launch_bounds__(kBlock) void collect_kernel(CollectArgs a)
 {
@@ -21,7 +22,7 @@ __global__ __launch_bounds__(kBlock) void collect_kernel(CollectArgs a)
     const int tid = threadIdx.x, b = blockIdx.x;
     const uint64_t G = gridDim.x;
     const uint32_t ep = kernel_epoch(a);
-    bool ok = pe_barrier<false>(a, ep, kPhaseStart, b);
+    const bool ok = launch_start(a, ep);
     if (ok) {
         for (int k = 0; k < a.p; ++k) {
             const int j = (a.me + (b + k)) % a.p;
@@ -53,14 +54,13 @@ __global__ __launch_bounds__(kBlock) void collect_kernel(CollectArgs a)
         }
     }
     // No member returns while a peer may still read its source.
-    ok = ok && pe_barrier<false>(a, ep, kPhaseEnd, b);
-    if (b == 0 && tid == 0 && a.ret) *a.ret = ok ? 0 : 1;
-    kernel_epoch_done(a, ep);
+    launch_finish(a, ep);
 }
 
 // Prefix sum.  Phase 1: member c owns chunk c; for each element it folds the members' values in
 // team order and stores every member k's prefix into its own scratch row k (write-through).
-// Phase 2 (after the mid barrier): each member pulls its row of every chunk into dest.
+// Phase 2 (once every member has published its chunk): each member pulls its row of every
+// chunk into dest.
 // Items are 16-B vectors when every base is 16-B aligned (chunk sizes are multiples of 64
 // elements); the < 16 leftover elements of the last chunk go element by element.  For P in
 // {2, 4, 8} the P loads of an item are all issued before the first store (compile-time register
@@ -110,36 +110,54 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
     const int p = P > 0 ? P : a.p, me = a.me;
     const uint64_t ipc = a.items_per_chunk;
     const uint32_t ep = kernel_epoch(a);
-    bool ok = pe_barrier<false>(a, ep, kPhaseStart, b);
-    if (ok) {
+    bool ok = launch_start(a, ep);
+    {
+        // Phase 1, grabbed piece by piece (tiles of kT items of chunk me; the last piece also
+        // folds the < E leftover elements); the workgroup completing the last piece publishes
+        // "chunk me ready" to every member, itself included.
         const uint64_t cs = min((uint64_t) me * ipc, a.nelems), ce = min(cs + ipc, a.nelems);
         const uint64_t nI = (ce - cs) / E;
-        for (uint64_t t0 = (uint64_t) b * kT; t0 < nI; t0 += G * kT) {
-            const char *base[kMaxPes];
-            char *row[kMaxPes];
-            for (int k = 0; k < p; ++k) {
-                base[k] = uniform_ptr(a.src[k] + (cs + t0 * E) * sizeof(T));
-                row[k] = (char *) uniform_ptr(a.scratch[me] + ((uint64_t) k * ipc + t0 * E) * sizeof(T));
-            }
-#pragma unroll
-            for (int u = 0; u < H; ++u) {
-                const uint64_t e = (uint64_t) u * kBlock + tid;
-                scan_item_fold<T, I, P>(a, base, row, (uint32_t) (e * sizeof(I)), p, me, t0 + e < nI);
-            }
-        }
         const uint64_t tail = (ce - cs) - nI * E;  // < E elements, last chunk only
-        if (tail && b == (int) ((nI / kT) % G) && (uint64_t) tid < tail) {
-            const uint64_t el = nI * E + tid;
-            const char *base[kMaxPes];
-            char *row[kMaxPes];
-            for (int k = 0; k < p; ++k) {
-                base[k] = uniform_ptr(a.src[k] + (cs + nI * E) * sizeof(T));
-                row[k] = (char *) uniform_ptr(a.scratch[me] + ((uint64_t) k * ipc + nI * E) * sizeof(T));
+        const uint32_t npieces = (uint32_t) max<uint64_t>(1, (nI + kT - 1) / kT);
+        while (ok) {
+            const uint32_t piece = block_grab(a, kEpRsHead);
+            if (piece >= npieces) break;
+            const uint64_t t0 = (uint64_t) piece * kT;
+            if (t0 < nI) {
+                const char *base[kMaxPes];
+                char *row[kMaxPes];
+                for (int k = 0; k < p; ++k) {
+                    base[k] = uniform_ptr(a.src[k] + (cs + t0 * E) * sizeof(T));
+                    row[k] = (char *) uniform_ptr(a.scratch[me] + ((uint64_t) k * ipc + t0 * E) * sizeof(T));
+                }
+#pragma unroll
+                for (int u = 0; u < H; ++u) {
+                    const uint64_t e = (uint64_t) u * kBlock + tid;
+                    scan_item_fold<T, I, P>(a, base, row, (uint32_t) (e * sizeof(I)), p, me, t0 + e < nI);
+                }
             }
-            scan_item_fold<T, T, 0>(a, base, row, (uint32_t) ((el - nI * E) * sizeof(T)), p, me, true);
+            if (tail && piece == npieces - 1 && (uint64_t) tid < tail) {
+                const uint64_t el = nI * E + tid;
+                const char *base[kMaxPes];
+                char *row[kMaxPes];
+                for (int k = 0; k < p; ++k) {
+                    base[k] = uniform_ptr(a.src[k] + (cs + nI * E) * sizeof(T));
+                    row[k] = (char *) uniform_ptr(a.scratch[me] + ((uint64_t) k * ipc + nI * E) * sizeof(T));
+                }
+                scan_item_fold<T, T, 0>(a, base, row, (uint32_t) ((el - nI * E) * sizeof(T)), p, me, true);
+            }
+            drain_block();
+            if (tid == 0 && __hip_atomic_fetch_add(a.ep_ctr + kEpP1Done, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT) == npieces - 1) {
+                release_system();
+                push_flag(a, kPhaseMid, 0, ep, true);
+            }
         }
     }
-    ok = ok && pe_barrier<true>(a, ep, kPhaseMid, b);
+    // Phase 2 may start once every member's chunk is complete.  Every phase-1 piece was grabbed
+    // before any workgroup gets here, by workgroups that wait for nothing else: no residency
+    // coupling.
+    ok = ok && block_wait(a, ep, kPhaseMid, 0, -2);
     if (ok) {
         for (int k = 0; k < p; ++k) {
             const int c = (me + b + k) % p;  // rotated over the members' scratch (links)
@@ -169,9 +187,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
             }
         }
     }
-    ok = ok && pe_barrier<false>(a, ep, kPhaseEnd, b);
-    if (b == 0 && tid == 0 && a.ret) *a.ret = ok ? 0 : 1;
-    kernel_epoch_done(a, ep);
+    launch_finish(a, ep);
 }
 
 // xGMI measurement hook (bench.py xgmi_probe): the same one-wave, one-item-per-thread shape as
@@ -200,6 +216,22 @@ __global__ __launch_bounds__(kFaninBlock) void pull_probe_kernel(FaninArgs a)
     wt_store(make_rsrc(uniform_ptr(a.dst + first * sizeof(Item))), off, acc);
 }
 
+// Test / measurement hook (ishmemi_c_occupy): a workgroup of 1024 work-items holding 80 KiB of
+// LDS — two of them fill a CU's 160 KiB of LDS and 32 waves — that sleeps for `ticks` of
+// s_memrealtime (100 MHz) and exits: lets a test hold most CUs while a collective runs.  Every
+// wave leaves once the time is up (bounded).
+constexpr int kOccupyThreads = 1024;
+constexpr int kOccupyLdsWords = 80 * 1024 / 4;
+__global__ __launch_bounds__(kOccupyThreads) void occupy_kernel(uint64_t ticks, uint32_t *sink)
+{
+    __shared__ uint32_t lds[kOccupyLdsWords];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = threadIdx.x; i < kOccupyLdsWords; i += kOccupyThreads) lds[i] = (uint32_t) i;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+    __syncthreads();
+    if (sink && lds[(threadIdx.x * 17) % kOccupyLdsWords] == 0xFFFFFFFFu) *sink = 1;  // keeps LDS live
+}
+
 template <typename K, typename A>
 hipError_t launch_res(K kernel, const A &a, int grid, hipStream_t s)
 {
@@ -215,6 +247,13 @@ hipError_t launch_collect(const CollectArgs &a, int grid, hipStream_t s)
     if (a.unit == 16) return launch_res(collect_kernel<16>, a, grid, s);
     if (a.unit == 4) return launch_res(collect_kernel<4>, a, grid, s);
     return launch_res(collect_kernel<1>, a, grid, s);
+}
+
+hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s)
+{
+    if (grid < 1 || usec > 60ull * 1000 * 1000) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(occupy_kernel, dim3(grid), dim3(kOccupyThreads), 0, s, usec * 100ull, (uint32_t *) nullptr);
+    return hipGetLastError();
 }
 
 hipError_t launch_pull_probe(const FaninArgs &a, int policy, hipStream_t s)

@@ -14,20 +14,24 @@
 //     streamed once (the local combine unit; with k = 1 it is the p = 1 self-reduce copy).
 //   * allreduce_kernel: ONE launch per collective, direct reduce-scatter + all-gather across the
 //     team.  PE c folds chunk c of every member's source (pulled over xGMI with system-coherent
-//     loads) in canonical team order 0..p-1 and writes its own dest; after a per-workgroup
-//     barrier every PE pulls the other reduced chunks from the peers' dests.  Each PE's link
+//     loads) in canonical team order 0..p-1 and writes its own dest; as each segment of it is
+//     published every PE pulls it from that PE's dest.  Each PE's link
 //     ingress is 2(p-1)/p * B spread over p-1 links, vs (p-1) * B serialised over peers in the
 //     reference loop.  Folding in canonical order makes every PE's result bit-identical (the
 //     reference's results differ between PEs for FP, docs/source/collectives.rst:1241-1244) and
 //     equal to the reference's PE-0 result and to its tester's check pattern
 //     (test/unit/reduce_sum.cpp:203-224).
 //   * The barriers replace ishmemi_team_sync's psync counters (src/collectives/sync_impl.h:30-69)
-//     with epoch-tagged flags in fine-grained memory, paired per workgroup index: workgroup b
-//     of every PE processes the same tiles of every chunk, so a barrier between the workgroups
-//     with index b is all the ordering the data needs (no grid-wide sync).  All remote
-//     accesses are LOADS (pull), so no PE's L2 can hold stale copies of bytes a peer wrote.
+//     with epoch-tagged flags in fine-grained memory: one "started" flag per member, one
+//     "ready" flag per reduced segment (the RS -> AG hand-off) and one "done reading" flag per
+//     member, exchanged by whichever workgroup gets there; work is grabbed from per-launch
+//     counters, so no workgroup ever waits for a particular peer workgroup and the launch
+//     completes whatever part of the grid is resident.  All remote data accesses are LOADS
+//     (pull), so no PE's L2 can hold stale copies of bytes a peer wrote.
 #pragma once
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "kernels.h"
@@ -141,16 +145,19 @@ __device__ __forceinline__ void wt_store(__amdgpu_buffer_rsrc_t r, uint32_t off,
 }
 
 // Kernel epochs live on the device: every workgroup of a launch reads the team's counter at
-// its start (epoch = counter + 1, 0 skipped: it is the flags' initial value) and the last
-// workgroup to finish stores the new value.  Collectives of a team are stream-ordered, so the
-// next launch sees it; a captured hipGraph therefore replays with fresh epochs every time.
+// its start (epoch = counter + 1) and the last workgroup to finish stores the new value.
+// Collectives of a team are stream-ordered, so the next launch sees it; a captured hipGraph
+// therefore replays with fresh epochs every time.  0 is the flags' initial value and never an
+// epoch; at the wrap the sequence goes 0xFFFFFFFF -> 2, so consecutive epochs always differ in
+// parity (the small-message rings are indexed by epoch parity).
 template <typename A>
 __device__ __forceinline__ uint32_t kernel_epoch(const A &a)
 {
     __shared__ uint32_t s_ep;
     if (threadIdx.x == 0) {
-        uint32_t e = __hip_atomic_load(a.ep_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
-        s_ep = e == 0 ? 1u : e;
+        const uint32_t e =
+            __hip_atomic_load(a.ep_ctr + kEpEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+        s_ep = e == 0 ? 2u : e;
     }
     __syncthreads();
     return s_ep;
@@ -160,82 +167,164 @@ template <typename A>
 __device__ __forceinline__ void kernel_epoch_done(const A &a, uint32_t ep)
 {
     if (threadIdx.x == 0) {
-        if (__hip_atomic_fetch_add(a.ep_ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
+        if (__hip_atomic_fetch_add(a.ep_ctr + kEpDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
             gridDim.x - 1) {
-            __hip_atomic_store(a.ep_ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(a.ep_ctr, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.ep_ctr + kEpDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.ep_ctr + kEpEpoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
 
-__device__ __forceinline__ uint32_t *flag_slot(uint32_t *base, int phase, int block)
+__device__ __forceinline__ uint32_t *flag_slot(uint32_t *base, int phase, int slot)
 {
-    return base + ((size_t) phase * kMaxBlocks + (size_t) block) * kMaxPes;
+    return base + ((size_t) phase * kMaxBlocks + (size_t) slot) * kMaxPes;
 }
 
-// Pairwise barrier between the workgroups with index `block` on every team member.
-// Replaces ishmemi_team_sync (src/collectives/sync_impl.h:30-69): instead of p remote
-// fetch-adds on one psync word and a spin to `size`, member me stores the call's epoch into
-// its own slot of every peer's flag row, then polls its local row until every peer's slot
-// holds the epoch (wrap-safe compare).  Called by ALL threads of the block; returns false on
-// timeout (recorded in *err) so the caller can drain instead of hanging the GPU.
-template <bool RELEASE, typename A>
-__device__ bool pe_barrier(const A &a, uint32_t ep, int phase, int block)
+// One lane: store epoch `ep` into this member's slot of row (phase, slot) on every other member
+// (and on itself when `self`) — system-scope stores over xGMI into fine-grained memory.
+template <typename A>
+__device__ __forceinline__ void push_flag(const A &a, int phase, int slot, uint32_t ep, bool self)
 {
-    __shared__ int s_ok;
-    // Every storing wave drains its stores, then one wave publishes (Guideline 16, R1).
+    for (int j = 0; j < a.p; ++j) {
+        if (j == a.me && !self) continue;
+        uint32_t *f = flag_slot(j == a.me ? a.my_flags : a.peer_flags[j], phase, slot) + a.me;
+        __hip_atomic_store(f, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// All threads: every wave's stores (all payload stores are write-through sc0 sc1) are
+// acknowledged before the workgroup barrier (Guideline 16, R1).
+__device__ __forceinline__ void drain_block()
+{
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+}
+
+// One lane, before a hand-off flag: system-scope release.  Nothing of ours is dirty (write-through
+// payload stores), so it only orders the drained stores before the flag; the asm wait guards the
+// compiler dropping the wait after buffer_wbl2 (MI355X_MICROARCH.md, compiler hazard).
+__device__ __forceinline__ void release_system()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <typename A>
+__device__ __forceinline__ void launch_fail(const A &a, int phase)
+{
+    __hip_atomic_store(a.ep_ctr + kEpFail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_or(a.err, 1u << phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// All threads call.  Wave 0 polls row (phase, slot) of the local flag block until the slot of
+// every member selected by `who` holds `ep` or a later epoch (wrap-safe): who = -1 every other
+// member, -2 every member including this one, >= 0 that member only.  Bounded: false on timeout
+// (recorded in the team's error word) or once another workgroup of this launch has timed out.
+// No acquire instruction follows: every load of bytes another PE produced is a system-coherent
+// (sc0 sc1) load, which neither L1 nor a stale L2 line can satisfy; the wavefront fence only
+// keeps the compiler from hoisting those loads above the poll (cdna_hip_programming.md
+// Guideline 16).
+template <typename A>
+__device__ bool block_wait(const A &a, uint32_t ep, int phase, int slot, int who)
+{
+    __shared__ int s_ok;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        const int p = a.p, me = a.me;
-        if constexpr (RELEASE) {
-            // Only the mid barrier hands off bytes this launch wrote (the reduced chunk).  Those
-            // are stored system-coherent write-through (wt_store), so this system-scope release
-            // has no dirty lines of ours to write back; it orders them before the flag.  The asm
-            // wait guards against the compiler dropping the wait after buffer_wbl2
-            // (MI355X_MICROARCH.md, compiler hazard).  Start / end barriers hand off nothing
-            // written in this launch (sources were written back at the producer kernels' end).
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (lane == 0) {
-            for (int j = 0; j < p; ++j) {
-                if (j == me) continue;
-                __hip_atomic_store(flag_slot(a.peer_flags[j], phase, block) + me, ep,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-        uint32_t *row = flag_slot(a.my_flags, phase, block);
-        bool done = (lane >= p) || (lane == me);
-        bool timed_out = false;
+        bool done = lane >= a.p || (who == -1 && lane == a.me) || (who >= 0 && lane != who);
+        const uint32_t *row = flag_slot(a.my_flags, phase, slot);
+        bool ok = true;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (!__all(done)) {
+        for (uint32_t it = 0;; ++it) {
             if (!done) {
-                const uint32_t v =
-                    __hip_atomic_load(row + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint32_t v = __hip_atomic_load(row + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 done = (int32_t) (v - ep) >= 0;
             }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-                timed_out = true;
-                break;
+            if (__all(done)) break;
+            if ((it & 15) == 15) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+                    if (lane == 0) launch_fail(a, phase);
+                    ok = false;
+                    break;
+                }
+                if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                        a.ep_ctr + kEpFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0) {
+                    ok = false;
+                    break;
+                }
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(1);
         }
-        // No acquire instruction: every load of bytes another PE produced is a system-coherent
-        // (sc0 sc1) load, which neither L1 nor a non-coherent L2 line can satisfy; the wavefront
-        // fence only keeps the compiler from hoisting those loads above the poll
-        // (cdna_hip_programming.md Guideline 16).
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane == 0) {
-            s_ok = !timed_out;
-            if (timed_out)
-                __hip_atomic_fetch_or(a.err, 1u << phase, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (lane == 0) s_ok = ok;
     }
     __syncthreads();
     return s_ok != 0;
+}
+
+// All threads call: one returning device-scope add on a launch word, broadcast to the block
+// (the dequeue primitive of MI355X_MICROARCH.md's price list).
+template <typename A>
+__device__ __forceinline__ uint32_t block_grab(const A &a, int word)
+{
+    __shared__ uint32_t s_v;
+    __syncthreads();  // every thread has read the previous value
+    if (threadIdx.x == 0)
+        s_v = __hip_atomic_fetch_add(a.ep_ctr + word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return s_v;
+}
+
+// Start of a collective launch (replaces the start half of ishmemi_team_sync,
+// src/collectives/sync_impl.h:30-69).  The first workgroup to run announces the launch to every
+// other member — this member's source is final, since the launch runs after everything before it
+// on the stream — and every workgroup waits until every member has announced the same launch.
+// No workgroup waits for a particular peer workgroup, so residency never matters.
+template <typename A>
+__device__ bool launch_start(const A &a, uint32_t ep)
+{
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(a.ep_ctr + kEpStarted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        push_flag(a, kPhaseStart, 0, ep, false);
+    return block_wait(a, ep, kPhaseStart, 0, -1);
+}
+
+// End of a collective launch; every workgroup calls it once.  The last workgroup to finish
+// tells every member that this member has finished reading their memory and waits until every
+// member has said the same, so neither a member's next launch nor its caller can overwrite bytes
+// a peer still reads (the end half of ishmemi_team_sync).  It then ORs a failure into *ret
+// (the caller zeroed it before the call: sticky over the launches of one call), resets the
+// launch words and publishes the epoch.
+template <typename A>
+__device__ void launch_finish(const A &a, uint32_t ep)
+{
+    __shared__ int s_last;
+    drain_block();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(a.ep_ctr + kEpDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) push_flag(a, kPhaseEnd, 0, ep, false);
+    const bool ok = block_wait(a, ep, kPhaseEnd, 0, -1);
+    if (threadIdx.x == 0) {
+        uint32_t *w = a.ep_ctr;
+        const bool failed =
+            !ok || __hip_atomic_load(w + kEpFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        if (failed && a.ret) __hip_atomic_fetch_or(a.ret, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int k = kEpDone; k < kEpWords; ++k)
+            __hip_atomic_store(w + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w + kEpEpoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Standalone barrier of one workgroup (team_sync_kernel): member me stores the call's epoch into
+// its own slot of every peer's row, then polls its local row.
+template <typename A>
+__device__ bool pe_barrier(const A &a, uint32_t ep, int phase, int slot)
+{
+    drain_block();
+    if (threadIdx.x == 0) push_flag(a, phase, slot, ep, false);
+    return block_wait(a, ep, phase, slot, -1);
 }
 
 // One reduce-scatter tile for a compile-time team size P and load rotation R: slot k holds member
@@ -297,8 +386,81 @@ __device__ __forceinline__ void rs_tile_dispatch(const ReduceArgs &a, int rot, u
     }
 }
 
+// Run-time team size: the fold is rotated only where the op is order-insensitive (integers,
+// min, max — bit-identical in any order), otherwise loaded and folded in team order.
+template <typename T, int OP, bool VEC>
+__device__ __forceinline__ void rs_tile_any(const ReduceArgs &a, int rot, uint64_t t0, uint64_t ce,
+                                            uint64_t head_bytes)
+{
+    using Item = std::conditional_t<VEC, Vec<T>, T>;
+    constexpr uint64_t IB = sizeof(Item);
+    constexpr bool kOrderFree =
+        !(std::is_floating_point_v<T> && (OP == ISHMEMI_OP_SUM || OP == ISHMEMI_OP_PROD));
+    const int tid = threadIdx.x, p = a.p;
+    Item acc[kUnroll];
+    for (int k = 0; k < p; ++k) {
+        const int j = kOrderFree ? (rot + k) % p : k;
+        const char *base = uniform_ptr(a.src[j] + head_bytes + t0 * IB);
+        Item x[kUnroll];
+        if (j == a.me) {
+            const Item *lp = (const Item *) base;
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint64_t e = (uint64_t) u * kBlock + tid;
+                if (t0 + e < ce) x[u] = lp[e];
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint64_t e = (uint64_t) u * kBlock + tid;
+                if (t0 + e < ce) x[u] = cload<Item>(r, (uint32_t) (e * IB));
+            }
+        }
+        if (k == 0) {
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) acc[u] = x[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) acc[u] = op1<T, OP>(acc[u], x[u]);
+        }
+    }
+    const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + head_bytes + t0 * IB));
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint64_t e = (uint64_t) u * kBlock + tid;
+        if (t0 + e < ce) wt_store(dr, (uint32_t) (e * IB), acc[u]);
+    }
+}
+
+// Member c's chunk of the reduce-scatter partition, [begin, end) in items.
+__device__ __forceinline__ void chunk_of(const ReduceArgs &a, int c, uint64_t &cs, uint64_t &ce)
+{
+    cs = min((uint64_t) c * a.items_per_chunk, a.nitems);
+    ce = min(cs + a.items_per_chunk, a.nitems);
+}
+
+// Segments of a chunk of `len` items: at least one, so an empty chunk (tiny arrays) still
+// hands off its head / tail and a consumer never waits for a segment nobody publishes.
+__device__ __forceinline__ uint32_t nsegs(uint64_t len, uint64_t seg)
+{
+    return (uint32_t) max<uint64_t>(1, (len + seg - 1) / seg);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Multi-PE reduce-scatter + all-gather (one launch per collective).
+//   start    - launch_start: every member has announced this launch (sources final).
+//   RS       - workgroups grab segments of chunk `me` from a work counter, fold each segment of
+//              every member's source in canonical team order (peers via sc0 sc1 loads), store
+//              it write-through into own dest, drain, and push "segment s ready" to every peer.
+//   AG       - workgroups grab (peer j, segment s) items, round-robin over the peers so every
+//              link is busy, wait for j's "segment s ready" in the LOCAL flag row and pull it
+//              from j's dest.  In place, the AG store into chunk j overwrites bytes member j
+//              read in its RS of segment s, which it had finished before publishing s.
+//   finish   - launch_finish: the last workgroup exchanges "done reading" with every member.
+// Every workgroup grabs RS work before AG work, so any workgroup waiting in AG implies that all
+// RS segments are held by running workgroups that wait for nothing but the start flags: the
+// launch completes whatever subset of its grid (and of its peers' grids) is resident.
 // ---------------------------------------------------------------------------------------------
 template <typename T, int OP, bool VEC, int P>
 __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_kernel(ReduceArgs a)
@@ -306,71 +468,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
     using Item = std::conditional_t<VEC, Vec<T>, T>;
     constexpr uint64_t IB = sizeof(Item);
     const int tid = threadIdx.x;
-    const int b = blockIdx.x;
-    const uint64_t G = gridDim.x;
     const int p = a.p, me = a.me;
     const uint64_t head_bytes = VEC ? a.head * sizeof(T) : 0;
-    const uint32_t ep = kernel_epoch(a);
-    bool ok = pe_barrier<false>(a, ep, kPhaseStart, b);
-
-    // ---- reduce-scatter: fold chunk `me` of every member's source, canonical team order ----
-    // The LOAD order is rotated by workgroup index (rot = b mod p), so at any instant the
-    // workgroups of every PE read from all p members (all links) instead of every PE draining
-    // member 0 first, then member 1, ... in lock step.  The FOLD order stays canonical
-    // (0, 1, ..., p-1): for compile-time team sizes the p loads are staged in registers and
-    // folded by fold_any; at run-time sizes the loop is rotated only where the op is
-    // order-insensitive (integers, min, max — bit-identical in any order).
+    const uint64_t seg = a.seg_items;
     const bool one = a.oneshot != 0;
-    if (ok) {
-        const uint64_t cs = one ? 0 : min((uint64_t) me * a.items_per_chunk, a.nitems);
-        const uint64_t ce = one ? a.nitems : min(cs + a.items_per_chunk, a.nitems);
-        const int rot = b % p;
-        for (uint64_t t0 = cs + (uint64_t) b * kTile; t0 < ce; t0 += G * kTile) {
-            if constexpr (P > 0) {
-                rs_tile_dispatch<T, OP, VEC, P>(a, rot, t0, ce, head_bytes);
-            } else {
-                constexpr bool kOrderFree =
-                    !(std::is_floating_point_v<T> && (OP == ISHMEMI_OP_SUM || OP == ISHMEMI_OP_PROD));
-                Item acc[kUnroll];
-                for (int k = 0; k < p; ++k) {
-                    const int j = kOrderFree ? (rot + k) % p : k;
-                    const char *base = uniform_ptr(a.src[j] + head_bytes + t0 * IB);
-                    Item x[kUnroll];
-                    if (j == me) {
-                        const Item *lp = (const Item *) base;
-#pragma unroll
-                        for (int u = 0; u < kUnroll; ++u) {
-                            const uint64_t e = (uint64_t) u * kBlock + tid;
-                            if (t0 + e < ce) x[u] = lp[e];
-                        }
-                    } else {
-                        const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
-#pragma unroll
-                        for (int u = 0; u < kUnroll; ++u) {
-                            const uint64_t e = (uint64_t) u * kBlock + tid;
-                            if (t0 + e < ce) x[u] = cload<Item>(r, (uint32_t) (e * IB));
-                        }
-                    }
-                    if (k == 0) {
-#pragma unroll
-                        for (int u = 0; u < kUnroll; ++u) acc[u] = x[u];
-                    } else {
-#pragma unroll
-                        for (int u = 0; u < kUnroll; ++u) acc[u] = op1<T, OP>(acc[u], x[u]);
-                    }
-                }
-                const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + head_bytes + t0 * IB));
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const uint64_t e = (uint64_t) u * kBlock + tid;
-                    if (t0 + e < ce) wt_store(dr, (uint32_t) (e * IB), acc[u]);
-                }
-            }
+    const uint32_t ep = kernel_epoch(a);
+    bool ok = launch_start(a, ep);
+
+    // ---- reduce-scatter of chunk `me` (one-shot: the whole array) ----
+    uint64_t cs = 0, ce = a.nitems;
+    if (!one) chunk_of(a, me, cs, ce);
+    const uint32_t nseg = nsegs(ce - cs, seg);
+    while (ok) {
+        const uint32_t s = block_grab(a, kEpRsHead);
+        if (s >= nseg) break;
+        const uint64_t ss = cs + (uint64_t) s * seg, se = min(ss + seg, ce);
+        // Load order rotated by segment: concurrently folded segments read from all members
+        // (all links) at once; the fold order stays canonical 0..p-1.
+        const int rot = (int) (s % (uint32_t) p);
+        for (uint64_t t0 = ss; t0 < se; t0 += kTile) {
+            if constexpr (P > 0) rs_tile_dispatch<T, OP, VEC, P>(a, rot, t0, se, head_bytes);
+            else rs_tile_any<T, OP, VEC>(a, rot, t0, se, head_bytes);
         }
         // Unaligned head (owned by member 0) and tail (owned by member p-1; one-shot: both by
-        // every member), element-wise.  Descriptors are based at the region (offsets < 16 B),
-        // never at the array start (a > 2 GiB array would exceed the descriptor's range).
-        if (VEC && b == 0) {
+        // every member), element-wise, with segment 0.  Descriptors are based at the region
+        // (offsets < 16 B), never at the array start (a > 2 GiB array exceeds a descriptor).
+        if (VEC && s == 0) {
             const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
             for (int region = 0; region < 2; ++region) {
                 const bool owner = one || (region == 0 ? me == 0 : me == p - 1);
@@ -388,37 +511,48 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
                 wt_store(make_rsrc(uniform_ptr(a.dst + rbase)), off, acc);
             }
         }
+        if (!one) {
+            drain_block();
+            if (tid == 0) {
+                release_system();
+                push_flag(a, kPhaseMid, (int) s, ep, false);
+            }
+        }
     }
 
-    if (!one) ok = ok && pe_barrier<true>(a, ep, kPhaseMid, b);
-
-    // ---- all-gather: pull every other member's reduced chunk from its dest ----
+    // ---- all-gather: pull every other member's reduced segments from its dest ----
     if (ok && !one) {
-        for (int k = 0; k < p - 1; ++k) {
-            // Peer order rotated by workgroup index: at any instant the workgroups of this PE
-            // pull from all p-1 peers at once, i.e. over all p-1 xGMI links, instead of every
-            // workgroup draining the same peer (one link) before moving to the next.  The tiles
-            // a workgroup pulls are still exactly those its partner workgroup b produced.
-            const int j = (me + 1 + (b + k) % (p - 1)) % p;
-            const uint64_t cs = min((uint64_t) j * a.items_per_chunk, a.nitems);
-            const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
-            for (uint64_t t0 = cs + (uint64_t) b * kTile; t0 < ce; t0 += G * kTile) {
-                const __amdgpu_buffer_rsrc_t r =
-                    make_rsrc(uniform_ptr(a.dstp[j] + head_bytes + t0 * IB));
+        const uint32_t per_peer = nsegs(min(a.items_per_chunk, a.nitems), seg);  // chunk 0 is the largest
+        const uint32_t total = (uint32_t) (p - 1) * per_peer;
+        for (;;) {
+            const uint32_t i = block_grab(a, kEpAgHead);
+            if (i >= total) break;
+            const int j = (me + 1 + (int) (i % (uint32_t) (p - 1))) % p;
+            const uint32_t s = i / (uint32_t) (p - 1);
+            uint64_t js, je;
+            chunk_of(a, j, js, je);
+            if (s >= nsegs(je - js, seg)) continue;
+            if (!block_wait(a, ep, kPhaseMid, (int) s, j)) {
+                ok = false;
+                break;
+            }
+            const uint64_t ss = js + (uint64_t) s * seg, se = min(ss + seg, je);
+            for (uint64_t t0 = ss; t0 < se; t0 += kTile) {
+                const __amdgpu_buffer_rsrc_t r = make_rsrc(uniform_ptr(a.dstp[j] + head_bytes + t0 * IB));
                 Item x[kUnroll];
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u) {
                     const uint64_t k = (uint64_t) u * kBlock + tid;
-                    if (t0 + k < ce) x[u] = cload<Item>(r, (uint32_t) (k * IB));
+                    if (t0 + k < se) x[u] = cload<Item>(r, (uint32_t) (k * IB));
                 }
-                Item *dp = (Item *) (a.dst + head_bytes + t0 * IB);
+                const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + head_bytes + t0 * IB));
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u) {
                     const uint64_t k = (uint64_t) u * kBlock + tid;
-                    if (t0 + k < ce) dp[k] = x[u];
+                    if (t0 + k < se) wt_store(dr, (uint32_t) (k * IB), x[u]);
                 }
             }
-            if (VEC && b == 0) {
+            if (VEC && s == 0) {
                 const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
                 const uint64_t rbase = (j == 0 ? 0 : tail_off) * sizeof(T);
                 const bool do_head = (j == 0) && ((uint64_t) tid < a.head);
@@ -429,11 +563,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_ker
             }
         }
     }
-
-    // ---- end: peers have finished pulling from my dest before anyone returns ----
-    ok = ok && pe_barrier<false>(a, ep, kPhaseEnd, b);
-    if (b == 0 && tid == 0 && a.ret) *a.ret = ok ? 0 : 1;
-    kernel_epoch_done(a, ep);
+    launch_finish(a, ep);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -569,7 +699,8 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
             else memcpy(a.dst + off, &acc, valid);
         }
     }
-    if (a.ret && blockIdx.x == 0 && threadIdx.x == 0) *a.ret = ok ? 0 : 1;
+    // *ret was zeroed by the caller: any thread that failed marks it (sticky over launches).
+    if (!ok && a.ret) __hip_atomic_fetch_or(a.ret, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     kernel_epoch_done(a, ep);
 }
 
@@ -586,8 +717,9 @@ hipError_t ll_t(const LLArgs &a, hipStream_t s)
 __global__ __launch_bounds__(kBlock) void team_sync_kernel(ReduceArgs a)
 {
     const uint32_t ep = kernel_epoch(a);
-    const bool ok = pe_barrier<false>(a, ep, kPhaseSync, 0);
-    if (threadIdx.x == 0 && a.ret) *a.ret = ok ? 0 : 1;
+    const bool ok = pe_barrier(a, ep, kPhaseSync, 0);
+    if (threadIdx.x == 0 && !ok && a.ret)
+        __hip_atomic_fetch_or(a.ret, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     kernel_epoch_done(a, ep);
 }
 
@@ -596,23 +728,35 @@ __global__ __launch_bounds__(kBlock) void team_sync_kernel(ReduceArgs a)
 template <int OP, typename S, typename U>
 using Canon = std::conditional_t<(OP == ISHMEMI_OP_MAX || OP == ISHMEMI_OP_MIN), S, U>;
 
-// Workgroups of `kernel` that are resident at once on this device.  The per-workgroup barriers
-// need every workgroup's partners resident, so the multi-PE grid is clamped to this.  One block
-// per CU of margin: the occupancy API over-reports by one block per CU for SGPR-heavy 256-thread
-// kernels on ROCm 7.2 (MI355X_MICROARCH.md, residency).  Same binary + same GPU model on every
-// PE => the same clamp, hence the same grid, on every PE.
+// Workgroups of `kernel` that are resident at once on this device (cached per kernel address),
+// divided among the PEs sharing the device.  The collectives are correct with any residency of
+// their own grid (they grab work; nothing is paired); the clamp avoids launching workgroups that
+// would find no work left, and keeps co-located PEs' launches from crowding each other out.  One block per CU of margin:
+// the occupancy API over-reports by one block per CU for SGPR-heavy 256-thread kernels on
+// ROCm 7.2 (MI355X_MICROARCH.md, residency).
+inline int resident_blocks_of(const void *kernel)
+{
+    static std::mutex mu;
+    static std::map<const void *, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(kernel);
+    if (it != cache.end()) return std::max(1, it->second / device_share());
+    int dev = 0, cus = 0, per = 0;
+    (void) hipGetDevice(&dev);
+    (void) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess) {
+        (void) hipGetLastError();
+        per = 1;
+    }
+    const int n = std::max(1, (per > 1 ? per - 1 : 1) * std::max(cus, 1));
+    cache[kernel] = n;
+    return std::max(1, n / device_share());
+}
+
 template <typename K>
 int resident_blocks(K kernel)
 {
-    static int cached = -1;
-    if (cached < 0) {
-        int dev = 0, cus = 0, per = 0;
-        (void) hipGetDevice(&dev);
-        (void) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess) per = 1;
-        cached = std::max(1, (per > 1 ? per - 1 : 1) * std::max(cus, 1));
-    }
-    return cached;
+    return resident_blocks_of((const void *) kernel);
 }
 
 template <typename K>

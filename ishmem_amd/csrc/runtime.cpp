@@ -87,6 +87,7 @@ struct Team {
 
 struct PeRecord {
     int32_t pe, pid, device, flags_fine_grained;
+    char pci_bus[32];  // identifies the physical GPU across processes
     uint64_t heap_size;
     // Launch-shape parameters: the multi-PE kernels pair workgroup b with workgroup b of every
     // peer and choose the LL path per call, so every PE must use the same values.
@@ -115,7 +116,7 @@ struct State {
     uint32_t *err_dev = nullptr;
     ishmemi_c_device_ctx_t *dctx = nullptr;  // device copy of the device-API context
     uint32_t *dev_epochs = nullptr;
-    uint32_t *kern_ep = nullptr;  // [team][2] kernel-epoch counters of the host-launched kernels
+    uint32_t *kern_ep = nullptr;  // [team][kEpWords] launch words of the host-launched kernels
 
     char *team_scratch = nullptr;  // small symmetric buffer for team-management collectives
     char *staging = nullptr;  // symmetric staging region for non-heap / host buffers
@@ -228,7 +229,7 @@ void heap_free(State &s, void *p)
 // ---------------- launch planning ----------------------------------------------------------
 struct Plan {
     bool vec;
-    uint64_t head, nitems, tail, items_per_chunk;
+    uint64_t head, nitems, tail, items_per_chunk, seg_items;
     int grid;
 };
 
@@ -239,6 +240,17 @@ uint64_t items_per_chunk(uint64_t nitems, int npes)
     const uint64_t per = (nitems + (uint64_t) npes - 1) / (uint64_t) npes;
     return std::max<uint64_t>(64, (per + 63) & ~uint64_t(63));
 }
+
+// Reduce-scatter segment (the unit of work grabbing and of the RS -> AG hand-off): whole tiles,
+// at most kMaxBlocks segments per chunk (one "ready" flag slot each).
+constexpr uint64_t kTileItems = (uint64_t) kBlock * kUnroll;
+uint64_t seg_items(uint64_t chunk_items)
+{
+    const uint64_t per = (chunk_items + kMaxBlocks - 1) / kMaxBlocks;
+    return std::max<uint64_t>(kTileItems, (per + kTileItems - 1) / kTileItems * kTileItems);
+}
+
+uint64_t nsegs(uint64_t len, uint64_t seg) { return std::max<uint64_t>(1, (len + seg - 1) / seg); }
 
 Plan make_plan(const void *dst, const void *const *srcs, int nsrc, size_t n, size_t es, int npes,
                int max_blocks, int max_grid)
@@ -262,10 +274,14 @@ Plan make_plan(const void *dst, const void *const *srcs, int nsrc, size_t n, siz
         pl.nitems = n;
         pl.tail = 0;
     }
-    const uint64_t tile = (uint64_t) kBlock * kUnroll;
     if (npes > 1) {
+        // Workgroups: enough for the larger of the two phases' work lists (RS segments of one
+        // chunk; AG items = p-1 peers x segments), capped; the kernel grabs work, so any grid
+        // size is correct.
         pl.items_per_chunk = items_per_chunk(pl.nitems, npes);
-        const uint64_t g = (pl.items_per_chunk + tile - 1) / tile;
+        pl.seg_items = seg_items(pl.items_per_chunk);
+        const uint64_t ns = nsegs(std::min(pl.items_per_chunk, pl.nitems), pl.seg_items);
+        const uint64_t g = std::max<uint64_t>(ns, (uint64_t) (npes - 1) * ns);
         pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t) max_blocks));
     } else {
         pl.items_per_chunk = pl.nitems;
@@ -293,7 +309,7 @@ int team_args(State &s, int team, ReduceArgs &a, std::string &why)
             return 1;
         }
     }
-    a.ep_ctr = s.kern_ep + 2 * team;
+    a.ep_ctr = s.kern_ep + (size_t) kEpWords * team;
     return 0;
 }
 
@@ -424,7 +440,7 @@ int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, si
     a.ret = ret;
     a.nbytes = bytes;
     a.timeout_ticks = (uint64_t) s.timeout_ms * 100000ull;
-    a.ep_ctr = s.kern_ep + 2 * team;
+    a.ep_ctr = s.kern_ep + (size_t) kEpWords * team;
     a.p = t.size;
     a.me = t.my_idx;
     HIP_TRY(launch_ll(op, dt, a, st));
@@ -456,17 +472,18 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     a.nitems = pl.nitems;
     a.tail = pl.tail;
     a.items_per_chunk = pl.items_per_chunk;
-    // Two members: reduce-scatter + all-gather moves B over the one link in two halves around a
-    // mid barrier; a one-shot fold of the whole array moves the same B with one barrier less.
+    a.seg_items = pl.seg_items;
+    // Two members: reduce-scatter + all-gather moves B over the one link in two halves with a
+    // hand-off between; a one-shot fold of the whole array moves the same B with no hand-off.
     // Not in place (a member would overwrite its source while the peer still reads it).  The
     // choice depends only on symmetric-address properties, so every member makes the same one.
     const uintptr_t d0 = (uintptr_t) dst, s0 = (uintptr_t) src, nb = n * es;
     if (t.size == 2 && (long long) nb <= s.oneshot_p2 && (d0 + nb <= s0 || s0 + nb <= d0)) {
         a.oneshot = 1;
         a.items_per_chunk = pl.nitems;
-        const uint64_t tile = (uint64_t) kBlock * kUnroll;
-        pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((pl.nitems + tile - 1) / tile,
-                                                                   (uint64_t) s.max_blocks));
+        a.seg_items = seg_items(pl.nitems);
+        pl.grid = (int) std::max<uint64_t>(
+            1, std::min<uint64_t>(nsegs(pl.nitems, a.seg_items), (uint64_t) s.max_blocks));
     }
     HIP_TRY(launch_allreduce(op, dt, pl.vec, a, pl.grid, st));
     return 0;
@@ -582,9 +599,9 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
     if (team < 0 || team >= kMaxTeams || !s.teams[team].valid || s.teams[team].my_idx < 0)
         return fail("fcollect: invalid team or caller not a member");
     Team &t = s.teams[team];
+    if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));  // sticky: launches OR failures in
     if (t.size == 1) {
         if (nbytes && dst != src && launch_copy(dst, src, nbytes, st)) return 1;
-        if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
     } else {
         if (!in_heap(s, dst)) return fail("fcollect: dest must be symmetric-heap memory");
         uint64_t nb[kMaxPes];
@@ -610,10 +627,10 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
         return fail("scan: invalid team or caller not a member");
     Team &t = s.teams[team];
     const size_t es = dtype_size(dt);
+    if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));  // sticky over the segments
     if (t.size == 1) {  // inclusive: the source; exclusive: the sum of nothing
         if (n && inclusive && dst != src && launch_copy(dst, src, n * es, st)) return 1;
         if (n && !inclusive) HIP_TRY(hipMemsetAsync(dst, 0, n * es, st));
-        if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
     } else if (n == 0) {
         if (team_sync_locked(s, team, st, ret)) return 1;
     } else {
@@ -683,6 +700,8 @@ int reduce_impl(int team, int op, int dt, void *dst, const void *src, size_t n, 
     if (n > 0 && (!dst || !src)) return fail("reduce: null buffer");
     const size_t es = dtype_size(dt);
     const size_t bytes = n * es;
+    // *ret: zeroed once here; every launch of the call ORs a failure into it (sticky).
+    if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
 
     if (t.size == 1) {
         // One PE: the reduction is a copy (reduce_impl.h:288-289 with no peers to fold).
@@ -696,7 +715,6 @@ int reduce_impl(int team, int op, int dt, void *dst, const void *src, size_t n, 
                 return 1;
             }
         }
-        if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
     } else if (n == 0) {
         // The reference still synchronises the team (reduce_impl.h:244, :254).
         if (team_sync_locked(s, team, st, ret)) return 1;
@@ -758,6 +776,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         return fail("init: invalid pe/npes (npes must be 1.." + std::to_string(kMaxPes) + ")");
     s.pe = pe;
     s.npes = npes;
+    set_device_share(1);
     s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, env_ll("ISHMEM_MAX_BLOCKS", kMaxBlocks)));
     s.timeout_ms = std::max<long long>(1, env_ll("ISHMEM_TIMEOUT_MS", 60000));
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
@@ -806,8 +825,12 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.peer_flags[pe] = s.flags;
 
     if (npes > 1) {
-        // Let peers import our dma-buf handles (pidfd_getfd needs ptrace rights under Yama).
-        prctl(PR_SET_PTRACER, PR_SET_PTRACER_ANY, 0, 0, 0);
+        // Let peers import our dma-buf handles (pidfd_getfd needs ptrace rights under Yama), for
+        // the import window only: the guard restores the default when this block is left.
+        struct PtracerWindow {
+            PtracerWindow() { prctl(PR_SET_PTRACER, PR_SET_PTRACER_ANY, 0, 0, 0); }
+            ~PtracerWindow() { prctl(PR_SET_PTRACER, 0, 0, 0, 0); }
+        } ptracer_window;
         std::string err;
         if (s.boot.attach(pe, npes, key, (int) std::max<long long>(s.timeout_ms, 10000), err))
             return fail(err);
@@ -821,6 +844,10 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.ll_max_bytes = s.ll_max_bytes;
         mine.oneshot_p2 = s.oneshot_p2;
         mine.staging_bytes = s.staging_bytes;
+        if (hipDeviceGetPCIBusId(mine.pci_bus, sizeof(mine.pci_bus), s.device) != hipSuccess) {
+            (void) hipGetLastError();
+            snprintf(mine.pci_bus, sizeof(mine.pci_bus), "dev%d", s.device);
+        }
         HIP_TRY(hipIpcGetMemHandle(&mine.heap_handle, s.heap));
         if (hipIpcGetMemHandle(&mine.flags_handle, s.flags) != hipSuccess) {
             // Uncached allocations that cannot be exported: fall back to coarse-grained flags
@@ -837,14 +864,18 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         }
         PeRecord all[kMaxPes];
         if (s.boot.allgather(&mine, all, sizeof(PeRecord), err)) return fail(err);
-        // Agree on the launch-shape parameters (the minimum over the PEs), so a per-process
-        // environment difference cannot pair mismatched grids or split LL from RS/AG.
+        // Agree on the parameters that choose a call's kernel (the minimum over the PEs), so a
+        // per-process environment difference cannot split LL from RS/AG or one-shot from RS/AG.
+        // The grid cap (max_blocks) stays per PE: the kernels grab work, nothing is paired.
         for (int j = 0; j < npes; ++j) {
-            s.max_blocks = (int) std::min<int64_t>(s.max_blocks, all[j].max_blocks);
             s.ll_max_bytes = std::min<long long>(s.ll_max_bytes, all[j].ll_max_bytes);
             s.oneshot_p2 = std::min<long long>(s.oneshot_p2, all[j].oneshot_p2);
             s.staging_bytes = std::min<size_t>(s.staging_bytes, all[j].staging_bytes);
         }
+        int share = 0;
+        for (int j = 0; j < npes; ++j)
+            share += strncmp(all[j].pci_bus, mine.pci_bus, sizeof(mine.pci_bus)) == 0;
+        set_device_share(share);
         for (int j = 0; j < npes; ++j) {
             if (j == pe) continue;
             if (all[j].heap_size != s.heap_size)
@@ -902,7 +933,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
                 HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_flags[j], hs[j], hipIpcMemLazyEnablePeerAccess));
             }
         }
-        if (s.boot.barrier(err)) return fail(err);
+        if (s.boot.barrier(err)) return fail(err);  // every peer has imported our handles
     }
 
     // Teams: WORLD, SHARED, NODE all span the node (src/teams.cpp:108-257).
@@ -921,12 +952,12 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.team_scratch = (char *) heap_alloc(s, kHeapAlign, kHeapAlign);
     if (!s.team_scratch) return 1;
     HIP_TRY(hipMalloc((void **) &s.dctx, sizeof(ishmemi_c_device_ctx_t)));
-    if (hipExtMallocWithFlags((void **) &s.kern_ep, 2 * kMaxTeams * sizeof(uint32_t), hipDeviceMallocUncached) !=
-        hipSuccess) {
+    const size_t ep_bytes = (size_t) kEpWords * kMaxTeams * sizeof(uint32_t);
+    if (hipExtMallocWithFlags((void **) &s.kern_ep, ep_bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void) hipGetLastError();
-        HIP_TRY(hipMalloc((void **) &s.kern_ep, 2 * kMaxTeams * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc((void **) &s.kern_ep, ep_bytes));
     }
-    HIP_TRY(hipMemset(s.kern_ep, 0, 2 * kMaxTeams * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(s.kern_ep, 0, ep_bytes));
     HIP_TRY(hipMalloc((void **) &s.dev_epochs, kMaxTeams * sizeof(uint32_t)));
     HIP_TRY(hipMemset(s.dev_epochs, 0, kMaxTeams * sizeof(uint32_t)));
     if (sync_device_ctx(s)) return 1;
@@ -938,8 +969,12 @@ std::string default_key()
 {
     if (const char *k = getenv("ISHMEM_BOOTSTRAP_KEY")) return k;
     std::string key = "job";
-    if (const char *p = getenv("MASTER_PORT")) key += std::string("_p") + p;
-    if (const char *r = getenv("TORCHELASTIC_RUN_ID")) key += std::string("_") + r;
+    const char *port = getenv("MASTER_PORT"), *run = getenv("TORCHELASTIC_RUN_ID");
+    if (port) key += std::string("_p") + port;
+    if (run) key += std::string("_") + run;
+    // No launcher variables: the PEs of one job are siblings (started by one launcher process),
+    // so its pid keeps concurrent jobs on a node apart.
+    if (!port && !run) key += "_pp" + std::to_string((long) getppid());
     return key;
 }
 
@@ -1179,7 +1214,7 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
             hipMemset(dev_flags(s.flags) + (size_t) slot * kDevFlagWordsPerTeam, 0,
                       kDevFlagWordsPerTeam * 4) != hipSuccess ||
             hipMemset(s.dev_epochs + slot, 0, sizeof(uint32_t)) != hipSuccess ||
-            hipMemset(s.kern_ep + 2 * slot, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
+            hipMemset(s.kern_ep + (size_t) kEpWords * slot, 0, kEpWords * sizeof(uint32_t)) != hipSuccess ||
             hipMemset(ll_ring(s.flags, slot), 0, kLLTeamBytes) != hipSuccess)
             return fail("team_split_strided: flag reset failed");
         if (sync_device_ctx(s)) return 1;
@@ -1303,6 +1338,12 @@ int ishmemi_c_pull_probe(void *dst, const void *const *srcs, int nsrc, size_t nb
     return 0;
 }
 
+int ishmemi_c_occupy(int grid, unsigned long long usec, void *stream)
+{
+    HIP_TRY(launch_occupy(grid, (uint64_t) usec, (hipStream_t) stream));
+    return 0;
+}
+
 int ishmemi_c_fcollect(int team, void *dest, const void *source, size_t nbytes)
 {
     return fcollect_impl(team, dest, source, nbytes, nullptr, 0, true);
@@ -1384,6 +1425,16 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "debug") return s.debug;
     if (n == "flags_fine_grained") return s.flags_fine_grained ? 1 : 0;
     if (n == "staging_bytes") return (long long) s.staging_bytes;
+    if (n == "heap_bytes") return (long long) s.heap_size;
+    if (n == "cu_count") {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+            (void) hipGetLastError();
+            return -1;
+        }
+        return cus;
+    }
     return -1;
 }
 

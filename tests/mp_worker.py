@@ -9,12 +9,42 @@ as strings through the queue.
 from __future__ import annotations
 
 import os
+import time
 import traceback
 from pathlib import Path
 
 import numpy as np
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def closed_form(op: str, npd, npes: int, idx: np.ndarray) -> np.ndarray:
+    """Reduce over PEs of x_pe[i] = (i mod 1024) + pe (exact in every type: int32 prod wraps,
+    f64 prod of <= 8 factors below 2^10 each is exact)."""
+    base = idx % 1024
+    if op == "min":
+        return base.astype(npd)
+    if op == "max":
+        return (base + npes - 1).astype(npd)
+    if op == "sum":
+        return (base * npes + npes * (npes - 1) // 2).astype(npd)
+    if npd is np.float64:
+        acc = base.astype(np.float64)
+        for pe in range(1, npes):
+            acc = acc * (base.astype(np.float64) + pe)
+        return acc
+    acc = base.astype(np.uint32)
+    for pe in range(1, npes):
+        acc = (acc * (base + pe).astype(np.uint32)).astype(np.uint32)
+    return acc.view(np.int32)
+
+
+def upload_closed_form(hip, ptr: int, npd, pe: int, n: int, chunk: int = 1 << 26) -> None:
+    """x_pe[i] = (i mod 1024) + pe, uploaded in chunks (no n-sized host temporaries)."""
+    for lo in range(0, n, chunk):
+        m = min(chunk, n - lo)
+        x = ((np.arange(lo, lo + m, dtype=np.int64) % 1024) + pe).astype(npd)
+        hip.upload(ptr + lo * np.dtype(npd).itemsize, x)
 
 
 def _bits_equal(a, b):
@@ -44,6 +74,14 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 bad = np.nonzero(got.view(np.uint8) != ref.view(np.uint8))[0]
                 fails.append(f"pe{pe} {tag}: {len(bad)} bytes differ from oracle (first byte {bad[:3]})")
                 return
+            if dt >= 8 and op in (OPS["sum"], OPS["prod"]) and len(srcs) > 1:
+                # The reference's own result on THIS PE folds self first, then team order
+                # (reduce_impl.h:247-253).  Both folds lie within fp_tolerance of the exact
+                # value, so they differ by at most twice that bound.
+                own = oracle.reduce_fold(op, dt, srcs, pe)
+                tol = 2.0 * oracle.fp_tolerance(dt, op, srcs, ref)
+                if not np.all(np.abs(own.astype(np.float64) - got.astype(np.float64)) <= tol):
+                    fails.append(f"pe{pe} {tag}: outside tolerance of the reference's PE-{pe} fold")
             if golden is not None:
                 if dt >= 8 and op in (OPS["sum"], OPS["prod"]):
                     tol = oracle.fp_tolerance(dt, op, srcs, ref)
@@ -59,6 +97,7 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             # job ends here, as after any collective error.
             ish.set_param("timeout_ms", 300)
             s_b, d_b = heap(1 << 20, DT["float"]), heap(1 << 20, DT["float"])
+            ret = ish.ishmem_malloc(4)
             if pe == 0:
                 for n in (100, 1 << 20):
                     r = ish.ishmem_float_sum_reduce(d_b, s_b, n)
@@ -69,6 +108,21 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                         fails.append(f"pe0 n={n}: unexpected error text: {msg}")
                 if ish.lib().ishmemi_c_error_count() != 2:
                     fails.append(f"pe0 error_count {ish.lib().ishmemi_c_error_count()} != 2")
+                # On-stream form with a multi-workgroup grid: *ret must report the failure (every
+                # failing workgroup ORs into it), also when the call spans several staged chunks.
+                st = hip.stream_create()
+                for n, host in ((1 << 20, False), (20_000_000, True)):  # host: two 64 MiB staged chunks
+                    hip.memset(ret, 0, 4)
+                    if host:
+                        hs, hd = np.zeros(n, np.float32), np.zeros(n, np.float32)
+                        ish.set_param("timeout_ms", 100)
+                        r = ish.ishmemx_float_sum_reduce_on_stream(hd.ctypes.data, hs.ctypes.data, n, ret, st)
+                    else:
+                        r = ish.ishmemx_float_sum_reduce_on_stream(d_b, s_b, n, ret, st)
+                    hip.stream_synchronize(st)
+                    if int(hip.download(ret, 1, np.int32)[0]) == 0 and r == 0:
+                        fails.append(f"pe0 on_stream n={n} host={host}: *ret is 0 after a timed-out launch")
+                hip.stream_destroy(st)
             ish.ishmem_finalize()
             q.put((pe, fails))
             return
@@ -370,6 +424,122 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                         fails.append(f"pe{pe} huge: wrong values near element {lo}")
             ish.ishmem_free(d_base)
             ish.ishmem_free(s_base)
+
+        if "occupied" in scenarios:
+            # Residency independence: PE 0 first enqueues, on another stream, a kernel holding all
+            # but 16 CUs (two 1024-work-item, 80 KiB-LDS workgroups per CU) for 4 s; then the PEs
+            # run a 64 MiB f32 sum, PE 0 with a 1024-workgroup grid of which only a fraction can
+            # be resident, the others with 16 workgroups (all PEs share this one GPU: a peer's
+            # full grid of waiting workgroups would otherwise take the free CUs PE 0 needs, which
+            # cannot happen across GPUs).  Nothing in the collective pairs workgroups across PEs,
+            # so it completes on the free CUs, correct, long before the occupying kernel ends.
+            ish.set_param("max_blocks", 1024 if pe == 0 else 16)
+            n = 16 << 20
+            ins = [oracle.fill_random(DT["float"], 0x0CC + j, n) for j in range(npes)]
+            s, d = heap(n, DT["float"]), heap(n, DT["float"])
+            ret = ish.ishmem_malloc(4)
+            hip.upload(s, ins[pe])
+            hip.memset(ret, 0x7F, 4)
+            occ, st = hip.stream_create(), hip.stream_create()
+            ish.ishmem_barrier_all()
+            if pe == 0:
+                cus = int(ish.get_param("cu_count"))
+                if ish.occupy(2 * max(1, cus - 16), 4_000_000, occ) != 0:
+                    fails.append(f"pe0 occupy failed {ish.last_error()}")
+                time.sleep(0.05)  # the occupying workgroups are resident before the reduce starts
+            t0 = time.perf_counter()
+            r = ish.ishmemx_float_sum_reduce_on_stream(d, s, n, ret, st)
+            hip.stream_synchronize(st)
+            dt_s = time.perf_counter() - t0
+            rv = int(hip.download(ret, 1, np.int32)[0])
+            if r or rv:
+                fails.append(f"pe{pe} occupied: rc={r} ret={rv} {ish.last_error()}")
+            else:
+                check("occupied", OPS["sum"], DT["float"], ins, hip.download(d, n, np.float32))
+            if dt_s > 3.0:
+                fails.append(f"pe{pe} occupied: reduce took {dt_s:.2f} s, i.e. it waited for the occupied CUs")
+            hip.stream_synchronize(occ)
+            hip.stream_destroy(occ)
+            hip.stream_destroy(st)
+            for b_ in (ret, d, s):
+                ish.ishmem_free(b_)
+            ish.set_param("max_blocks", int(os.environ.get("ISHMEM_MAX_BLOCKS", 1024)))
+
+        if "tripwire" in scenarios:
+            from ishmem_amd import selfcheck
+            res = selfcheck.chain_tripwire(ish, hip, pe, npes, nmax=int(os.environ.get("TRIPWIRE_N", 1 << 20)),
+                                           iters=int(os.environ.get("TRIPWIRE_ITERS", 12)))
+            if not res["checked"]:
+                fails.append(f"pe{pe} tripwire: {res}")
+
+        if "cfg4" in scenarios:
+            # BASELINE configs[3] at its own size: float32 sum-reduce of 1 GiB per PE, every word of
+            # dest compared with the closed form on every PE.
+            n = 256 << 20
+            s, d = ish.ishmem_malloc(n * 4), ish.ishmem_malloc(n * 4)
+            if not (s and d):
+                raise RuntimeError(f"cfg4 heap: {ish.last_error()}")
+            upload_closed_form(hip, s, np.float32, pe, n)
+            r = ish.ishmem_float_sum_reduce(d, s, n)
+            if r:
+                fails.append(f"pe{pe} cfg4 rc={r} {ish.last_error()}")
+            else:
+                bad = 0
+                for lo in range(0, n, 1 << 26):
+                    m = min(1 << 26, n - lo)
+                    want = closed_form("sum", np.float32, npes, np.arange(lo, lo + m, dtype=np.int64))
+                    bad += int(np.count_nonzero(hip.download(d + 4 * lo, m, np.float32) != want))
+                if bad:
+                    fails.append(f"pe{pe} cfg4: {bad} of {n} words wrong")
+            ish.ishmem_free(d)
+            ish.ishmem_free(s)
+
+        if "cfg5" in scenarios:
+            # BASELINE configs[4]: min / max / prod x int32 / float64 at 4 KiB * 4^k up to
+            # CFG5_MAX_BYTES (4 GiB) per PE.  Up to 64 MiB every word is compared; above, windows
+            # of 4096 elements at both edges of every member's chunk, the array's end and 16
+            # seeded random places (int: bit-exact; f64 min / max / prod of small integers: exact).
+            maxb = int(os.environ.get("CFG5_MAX_BYTES", 4 << 30))
+            rng = np.random.default_rng(55)
+            for dtn, npd in (("int32", np.int32), ("double", np.float64)):
+                es = np.dtype(npd).itemsize
+                nmax = maxb // es
+                s, d = ish.ishmem_malloc(maxb), ish.ishmem_malloc(maxb)
+                if not (s and d):
+                    raise RuntimeError(f"cfg5 heap: {ish.last_error()}")
+                upload_closed_form(hip, s, npd, pe, nmax)
+                for op in ("min", "max", "prod"):
+                    nb = 4096
+                    while nb <= maxb:
+                        n = nb // es
+                        hip.memset(d, 0xA5, nb)
+                        r = ish.reduce(op, dtn, d, s, n)
+                        if r:
+                            fails.append(f"pe{pe} cfg5 {op} {dtn} {nb} B rc={r} {ish.last_error()}")
+                            nb *= 4
+                            continue
+                        if nb <= (64 << 20):
+                            wins = [(0, n)]
+                        else:
+                            nitems = nb // 16
+                            wins = []
+                            for c in range(npes):
+                                b0, e0 = ish.chunk_bounds(nitems, npes, c)
+                                for edge in (b0, e0):
+                                    lo = max(0, edge * (16 // es) - 2048)
+                                    wins.append((lo, min(n, lo + 4096) - lo))
+                            wins.append((n - 4096, 4096))
+                            wins += [(int(x), 4096) for x in rng.integers(0, n - 4096, 16)]
+                        bad = 0
+                        for lo, m in wins:
+                            want = closed_form(op, npd, npes, np.arange(lo, lo + m, dtype=np.int64))
+                            got = hip.download(d + lo * es, m, npd)
+                            bad += int(np.count_nonzero(got.view(np.uint8) != want.view(np.uint8)))
+                        if bad:
+                            fails.append(f"pe{pe} cfg5 {op} {dtn} {nb} B: {bad} bytes wrong")
+                        nb *= 4
+                ish.ishmem_free(d)
+                ish.ishmem_free(s)
 
         if "collect" in scenarios:
             # fcollect.cpp / collect.cpp testers: per-PE word pattern, dest = the members' blocks

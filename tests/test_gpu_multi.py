@@ -4,6 +4,9 @@ the driver's).  Every PE checks its dest against the oracle bit-for-bit (canonic
 fold) and against MPICH's MPI_Allreduce golden output (ints / min / max bit-exact; FP sum/prod
 within (p-1)*u*sum|x_i| resp. (p-1)*u*|ref|)."""
 import multiprocessing as mp
+import queue
+import sys
+import time
 import uuid
 
 import pytest
@@ -25,9 +28,19 @@ def run_pes(npes: int, scenarios: list[str], timeout: float = 240.0, env: dict |
     for p in procs:
         p.start()
     results = {}
+    t0 = time.monotonic()
     try:
-        for _ in range(npes):
-            pe, fails = q.get(timeout=timeout)
+        while len(results) < npes:
+            # Heartbeat on stderr (run pytest with -s on the GPU box): a long multi-PE case stays
+            # visibly alive, and a PE that never reports ends the test at `timeout`.
+            try:
+                pe, fails = q.get(timeout=min(30.0, max(1.0, timeout - (time.monotonic() - t0))))
+            except queue.Empty:
+                if time.monotonic() - t0 >= timeout:
+                    break
+                print(f"[run_pes {npes} PEs {scenarios}] {time.monotonic() - t0:.0f} s, "
+                      f"{len(results)} reported", file=sys.stderr, flush=True)
+                continue
             results[pe] = fails
     finally:
         for p in procs:
@@ -110,3 +123,31 @@ def test_two_pe_reduce_scatter_allgather_path():
     # (and no LL) for the same golden / offset / large cases.
     run_pes(2, ["golden", "offsets", "large"],
             env={"ISHMEM_ONESHOT_P2_MAX_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_MAX_BLOCKS": 64})
+
+
+def test_reduce_completes_while_another_kernel_holds_most_cus():
+    # Weakness of the round-1 protocol (workgroup b of every PE paired with workgroup b of every
+    # peer): a collective whose partner workgroups cannot all be resident.  Now any workgroup may
+    # satisfy a start flag and work is grabbed, so the reduce runs on whatever CUs are free.
+    run_pes(2, ["occupied"], env={"ISHMEM_MAX_BLOCKS": 1024}, timeout=120)
+
+
+@pytest.mark.parametrize("npes", [2, 4, 8])
+def test_coherence_tripwire_chained_producer_reduce(npes):
+    # Producer kernel -> on-stream reduce, dest of step k = source of step k+1, alternating teams,
+    # offsets and sizes (LL and RS + AG), full window compared on every PE every iteration.
+    run_pes(npes, ["tripwire"], env={"ISHMEM_MAX_BLOCKS": 1024}, timeout=300)
+
+
+def test_config4_eight_pes_1GiB_f32_sum_full_compare():
+    # BASELINE configs[3] at its size on the one GPU: 8 PEs x 1 GiB, full default grid per PE
+    # (8 x 1024 workgroups oversubscribe the device: residency-independent protocol).
+    run_pes(8, ["cfg4"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "3G"}, timeout=600)
+
+
+@pytest.mark.parametrize("npes", [2, 8])
+def test_config5_min_max_prod_int32_f64_4KiB_to_4GiB(npes):
+    # BASELINE configs[4]: min/max/prod x int32/float64, 4 KiB * 4^k up to 4 GiB per PE, every
+    # chunk edge checked (4 GiB src + 4 GiB dest + staging per PE: a 9 GiB heap).
+    run_pes(npes, ["cfg5"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "9G",
+                                 "CFG5_MAX_BYTES": 4 << 30}, timeout=900)
