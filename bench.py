@@ -7,13 +7,21 @@
 N=1 (BASELINE configs[1]): ishmem_float_sum_reduce over a 1 GiB symmetric-heap array on one PE
 (reference semantics: dest = source, src/collectives/reduce_impl.h:288-289), plus the local
 combine unit dst = a + b (the per-step unit of the multi-PE path) at the same size.
-N>1 (launched by torch.distributed.run, one process per GPU): the same call over TEAM_WORLD =
-direct reduce-scatter + all-gather over xGMI (configs[2..3]); value = N * B / t (whole job).
+N>1 (configs[2..3]): one process per GPU; `python bench.py --gpus N` starts the N ranks itself
+(torch.distributed.run as a child process, before anything touches the GPU) unless a launcher
+already set WORLD_SIZE.  The same call over TEAM_WORLD = direct reduce-scatter + all-gather over
+xGMI.
 
 A "step" = one reduce of B bytes per PE, inputs already resident in HBM.  K steps are timed
-between barrier + device synchronize on both sides; ms_per_step is the max over ranks.  The
-dominant kernel's duration is measured with HIP events on the stream it runs on.  rank 0 at N=1
-also times the reference's host-proxy CPU reduce, restated in oracle/ (cpu_baseline).
+between barrier + device synchronize on both sides; ms_per_step is the max over ranks.
+  value       = N * B / t  (whole job: payload bytes of all PEs per second)
+  algbw_GiBps = B / t      (per PE, the reference harness's payload rate,
+                            test/include/ishmem_tester.h:1553-1555; SURVEY.md §8(d)'s targets)
+The dominant kernel's duration is measured with HIP events on the stream it runs on.  The timed
+dest is compared in full with the closed form on every rank.  Rank 0 (every rank at N>1) also
+times the reference's host path — 64 KiB chunks, each through a synchronous device->host copy, the
+MPI-style shared-memory allreduce over the p PEs and a synchronous host->device copy
+(reduce_impl.h:186-228, memory.cpp:310-321) — restated in oracle/ (cpu_baseline).
 """
 from __future__ import annotations
 
@@ -21,6 +29,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 import uuid
@@ -35,9 +45,58 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 # run with an error line within a minute instead of stalling every queued step for a minute each.
 os.environ.setdefault("ISHMEM_TIMEOUT_MS", "15000")
 
+METRIC = "GiB/s device-resident float32 sum-reduce at 1/2/4/8 PEs vs HBM+xGMI roofline"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 XGMI_LINK_GBS = 153.6       # per link, as given by the task brief (may be bidirectional)
 GiB = float(1 << 30)
+CFG5_MAX_BYTES = 4 << 30    # BASELINE configs[4]: 4 KiB .. 4 GiB per PE
+
+
+_OUT = None  # where the one JSON line goes (the original stdout; see main)
+
+
+def emit(line: dict) -> None:
+    out = _OUT if _OUT is not None else sys.stdout
+    out.write(json.dumps(line) + "\n")
+    out.flush()
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (rank 0), so a long leg is visibly alive; stdout keeps the one JSON line."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def host_info() -> dict:
+    """Core count and CPU model of the box, for the CPU baseline (nproc + lscpu)."""
+    model = None
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"nproc": os.cpu_count(), "usable_cores": usable, "cpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def self_launch(args) -> int:
+    """--gpus N > 1 without a launcher: run the N ranks as a child torch.distributed.run (never
+    exec: nothing here has touched the GPU, and the parent only relays), rank 0's JSON line
+    passes through on stdout; the exit code is the child's."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           str(Path(__file__).resolve()), *sys.argv[1:]]
+    log(f"self-launch: {' '.join(cmd[1:])}")
+    return subprocess.run(cmd).returncode
 
 
 def pmc_traffic(kernel_tag: str, nbytes: int):
@@ -55,35 +114,68 @@ def pmc_traffic(kernel_tag: str, nbytes: int):
     return None
 
 
-def config5_sweep(ish, hip, src, dst, nbytes_max, world, rank, dist, stream):
-    """Config 5: min/max/prod x int32/float64, 4 KiB .. nbytes_max (the bench payload, 1 GiB by
-    default) per PE in steps of 4x: us per call (max over ranks), algbw, last 256 results checked
-    against the closed form of x_pe[i] = (i mod 1024) + pe."""
+def closed_form(op: str, npd, world: int, idx: np.ndarray) -> np.ndarray:
+    """Reduce over PEs of x_pe[i] = (i mod 1024) + pe (exact in every type used here)."""
+    base = idx % 1024
+    if op == "min":
+        return base.astype(npd)
+    if op == "max":
+        return (base + world - 1).astype(npd)
+    if op == "sum":
+        return (base * world + world * (world - 1) // 2).astype(npd)
+    if npd is np.float64:
+        acc = base.astype(np.float64)
+        for pe in range(1, world):
+            acc = acc * (base.astype(np.float64) + pe)
+        return acc
+    acc = base.astype(np.uint32)
+    for pe in range(1, world):
+        acc = (acc * (base + pe).astype(np.uint32)).astype(np.uint32)
+    return acc.view(np.int32)
+
+
+def upload_closed_form(hip, ptr: int, npd, pe: int, n: int, chunk: int = 1 << 26) -> None:
+    for lo in range(0, n, chunk):
+        m = min(chunk, n - lo)
+        hip.upload(ptr + lo * np.dtype(npd).itemsize,
+                   ((np.arange(lo, lo + m, dtype=np.int64) % 1024) + pe).astype(npd))
+
+
+def full_check(hip, ptr: int, op: str, npd, world: int, n: int, chunk: int = 1 << 26) -> int:
+    """Words of dest[0:n] that differ from the closed form (every word compared)."""
+    bad = 0
+    es = np.dtype(npd).itemsize
+    for lo in range(0, n, chunk):
+        m = min(chunk, n - lo)
+        want = closed_form(op, npd, world, np.arange(lo, lo + m, dtype=np.int64))
+        got = hip.download(ptr + lo * es, m, npd)
+        bad += int(np.count_nonzero(got.view(np.uint8) != want.view(np.uint8)))
+    return bad
+
+
+def max_over_ranks(dist, vals: list[float]) -> list[float]:
+    if dist is None:
+        return vals
     import torch
+    t = torch.tensor(vals, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t]
+
+
+def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max):
+    """BASELINE configs[4]: min/max/prod x int32/float64, 4 KiB .. nbytes_max per PE in steps of 4x:
+    us per call (max over ranks), algbw, and a check of every word up to 64 MiB, above that of
+    4096-element windows at both edges of every member's chunk, the array's end and 8 seeded
+    random places, against the closed form of x_pe[i] = (i mod 1024) + pe."""
     out = []
+    rng = np.random.default_rng(5)
     for dtn, npd in (("int32", np.int32), ("double", np.float64)):
         es = np.dtype(npd).itemsize
         nmax = nbytes_max // es
-        x = (np.arange(nmax, dtype=np.int64) % 1024).astype(npd) + npd(rank)
-        hip.upload(src, x)
-        del x
-
-        def expect(op, idx):
-            base = idx % 1024
-            if op == "min":
-                return base.astype(npd)
-            if op == "max":
-                return (base + world - 1).astype(npd)
-            if npd is np.float64:
-                acc = base.astype(np.float64)
-                for pe in range(1, world):
-                    acc = acc * (base.astype(np.float64) + pe)
-                return acc
-            acc = base.astype(np.uint32)
-            for pe in range(1, world):
-                acc = (acc * (base + pe).astype(np.uint32)).astype(np.uint32)
-            return acc.view(np.int32)
-
+        src, dst = ish.ishmem_malloc(nbytes_max), ish.ishmem_malloc(nbytes_max)
+        if not (src and dst):
+            raise RuntimeError(f"config-5 sweep: {ish.last_error()}")
+        upload_closed_form(hip, src, npd, rank, nmax)
         for op in ("min", "max", "prod"):
             nb = 4096
             while nb <= nbytes_max:
@@ -100,17 +192,31 @@ def config5_sweep(ish, hip, src, dst, nbytes_max, world, rank, dist, stream):
                         raise RuntimeError(ish.last_error())
                 e1.record(stream)
                 hip.stream_synchronize(stream)
-                us = e0.elapsed_ms(e1) * 1000.0 / it
-                t = torch.tensor([us], dtype=torch.float64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                us = float(t[0])
-                k = min(n, 256)
-                got = hip.download(dst + (n - k) * es, k, npd)
-                want = expect(op, np.arange(n - k, n, dtype=np.int64))
-                ok = bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
+                us = max_over_ranks(dist, [e0.elapsed_ms(e1) * 1000.0 / it])[0]
+                if nb <= (64 << 20):
+                    wins = [(0, n)]
+                else:
+                    nitems = nb // 16
+                    wins = []
+                    for c in range(world):
+                        b0, e0_ = ish.chunk_bounds(nitems, world, c)
+                        for edge in (b0, e0_):
+                            lo = max(0, edge * (16 // es) - 2048)
+                            wins.append((lo, min(n, lo + 4096) - lo))
+                    wins.append((n - 4096, 4096))
+                    wins += [(int(x), 4096) for x in rng.integers(0, n - 4096, 8)]
+                bad = 0
+                for lo, m in wins:
+                    want = closed_form(op, npd, world, np.arange(lo, lo + m, dtype=np.int64))
+                    got = hip.download(dst + lo * es, m, npd)
+                    bad += int(np.count_nonzero(got.view(np.uint8) != want.view(np.uint8)))
+                bad = int(max_over_ranks(dist, [float(bad)])[0])
                 out.append({"op": op, "dtype": dtn, "bytes": nb, "us": round(us, 2),
-                            "algbw_GiBps": round(nb / GiB / (us * 1e-6), 2), "checked": ok})
+                            "algbw_GiBps": round(nb / GiB / (us * 1e-6), 2),
+                            "checked": bad == 0, "words_checked": sum(m for _, m in wins)})
                 nb *= 4
+        ish.ishmem_free(dst)
+        ish.ishmem_free(src)
     return out
 
 
@@ -122,7 +228,6 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
               resident capacity);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
       ll    - 4 / 16 / 64 KiB with the one-hop granule path on (default) and off."""
-    import torch
 
     def timed(n, iters):
         for _ in range(2):
@@ -136,9 +241,7 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
                 raise RuntimeError(ish.last_error())
         e1.record(stream)
         hip.stream_synchronize(stream)
-        t = torch.tensor([e0.elapsed_ms(e1) / iters], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t[0])
+        return max_over_ranks(dist, [e0.elapsed_ms(e1) / iters])[0]
 
     out = []
 
@@ -152,8 +255,7 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
         out.append({"case": case, param: value, "bytes": nbytes, "us": round(ms * 1e3, 2),
                     "algbw_GiBps": round(nbytes / GiB / (ms * 1e-3), 2)})
 
-    # Several PEs sharing one GPU (ISHMEM_BENCH_SAME_DEVICE rehearsals) must keep their summed
-    # grids resident, so there the sweep stays at or below the grid cap the run started with.
+    # Several PEs sharing one GPU (ISHMEM_BENCH_SAME_DEVICE rehearsals) keep the cap they started with.
     cap = ish.get_param("max_blocks") if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else 1024
     for mb in (128, 256, 512, 1024):
         if mb <= cap:
@@ -165,6 +267,49 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
         run("ll_on", "ll_max_bytes", 65536, nb, 50)
         run("ll_off", "ll_max_bytes", 0, nb, 50)
     return out
+
+
+def xgmi_probe(ish, hip, src, dst, B, world, rank, dist, stream, barrier):
+    """Measured link rates (report against the spec AND a measured L).  Plain
+    pulls of a peer's source through the local combine kernel, no barriers inside:
+      pull1   — every rank copies S bytes from rank+1 (ring: each link busy in one direction)
+      pullall — every rank folds the sources of all p-1 peers (ingress (p-1)*S per GPU)
+      push1   — every rank writes S bytes into rank+1's dest (remote stores)
+    pull1 / pullall load nontemporal; the *_sc twins issue the system-coherent (sc0 sc1) loads the
+    collectives use on peer memory."""
+    S = min(B, 256 << 20)
+    ns = S // 4
+    peers = [(rank + d) % world for d in range(1, world)]
+    probe = {}
+    cases = (("pull1", [ish.ishmem_ptr(src, peers[0])], dst, 0),
+             ("pull1_sc", [ish.ishmem_ptr(src, peers[0])], dst, 1),
+             ("pullall", [ish.ishmem_ptr(src, j) for j in peers], dst, 0),
+             ("pullall_sc", [ish.ishmem_ptr(src, j) for j in peers], dst, 1),
+             ("push1", [src], ish.ishmem_ptr(dst, peers[0]), None))
+
+    def launch(srcs, out, pol):
+        if pol is None:
+            return ish.combine("sum", "float", out, srcs, ns, stream)
+        return ish.pull_probe(out, srcs, S, pol, stream)
+
+    for name, srcs, out, pol in cases:
+        for _ in range(2):
+            launch(srcs, out, pol)
+        barrier()
+        k = 10
+        e0, e1 = hip.Event(), hip.Event()
+        e0.record(stream)
+        for _ in range(k):
+            if launch(srcs, out, pol) != 0:
+                raise RuntimeError(ish.last_error())
+        e1.record(stream)
+        hip.stream_synchronize(stream)
+        ms = max_over_ranks(dist, [e0.elapsed_ms(e1) / k])[0]
+        gbs = len(srcs) * S / (ms * 1e-3) / 1e9
+        probe[name] = {"bytes_per_peer": S, "peers": len(srcs), "ms": round(ms, 4),
+                       "ingress_GBps": round(gbs, 1), "per_link_GBps": round(gbs / len(srcs), 1)}
+    barrier()
+    return probe
 
 
 def rccl_allreduce(dist, device, n, B, world, steps, line, limit_s=240.0):
@@ -179,7 +324,7 @@ def rccl_allreduce(dist, device, n, B, world, steps, line, limit_s=240.0):
     def expire():
         if line is not None:
             line["rccl_allreduce"] = {"error": f"did not finish within {limit_s:.0f} s"}
-            print(json.dumps(line), flush=True)
+            emit(line)
         os._exit(0)
 
     wd = threading.Timer(limit_s, expire)
@@ -197,31 +342,87 @@ def rccl_allreduce(dist, device, n, B, world, steps, line, limit_s=240.0):
         for _ in range(steps):
             dist.all_reduce(buf, group=pg)
         torch.cuda.synchronize()
-        tr = time.perf_counter() - t0
-        tt = torch.tensor([tr], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        tr = float(tt[0])
+        tr = max_over_ranks(dist, [time.perf_counter() - t0])[0]
         buf.fill_(1.0)
         dist.all_reduce(buf, group=pg)
         ok = bool(torch.all(buf == float(world)).item())
         del buf
         torch.cuda.synchronize()
         dist.destroy_process_group(pg)
-        return {"value": world * B / GiB / (tr / steps), "unit": "GiB/s",
-                "ms_per_step": tr / steps * 1000.0, "steps": steps, "checked": ok}
+        return {"value": world * B / GiB / (tr / steps), "algbw_GiBps": B / GiB / (tr / steps),
+                "unit": "GiB/s", "ms_per_step": tr / steps * 1000.0, "steps": steps, "checked": ok}
     except Exception as ex:
         return {"error": str(ex)}
     finally:
         wd.cancel()
 
 
-def log(msg: str) -> None:
-    """Progress on stderr (rank 0), so a long leg is visibly alive; stdout keeps the one JSON line."""
-    if int(os.environ.get("RANK", "0")) == 0:
-        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+def cpu_baseline_leg(ish, hip, src, dst, n, B, world, rank, dist, key) -> tuple[dict, dict]:
+    """The reference's host path, restated in oracle/ and timed on the host cores
+    (reduce_impl.h:186-228 -> memory.cpp:310-321 -> runtime_mpi.cpp:802-812): every 64 KiB chunk
+    of the device source goes through a synchronous device->host hipMemcpy, the shared-memory
+    allreduce of the p PEs' chunks, and a synchronous host->device hipMemcpy.
+      N = 1: this PE alone over the full 1 GiB (p = 1), then p = 2 / 4 / 8 side by side on a
+             64 MiB sample (p - 1 helper processes with their own HIP buffers on this GPU, so
+             the p members share its PCIe link), the memcpy-only restatement, and BASELINE
+             configs[0] (int32 sum, 2 PEs, host loopback, no GPU).
+      N > 1: every rank on its own GPU, p = N, over a 64 MiB-per-PE sample of the payload (the
+             p-member exchange costs per chunk grow with p; the sample bounds the leg)."""
+    import oracle  # CPU baseline leg only: the reference's host path, restated (test infrastructure)
+    op, dt = oracle.OPS["sum"], oracle.DTYPES["float"]
+    extra = {}
+    if world > 1:
+        ns = min(n, (64 << 20) // 4)
+        t = oracle.host_bounce_time(op, dt, ns, rank, world, key + "cpu", src, dst, reps=1)
+        t = max_over_ranks(dist, [t])[0]
+        return ({"value": ns * 4 / GiB / t, "unit": "GiB/s", "cores": world, "kind": "port",
+                 "per": "per PE (B/t, compare algbw_GiBps)",
+                 "whole_job_GiBps": world * ns * 4 / GiB / t,
+                 "sample": f"{world} PEs x {ns * 4 >> 20} MiB f32 sum (a sample of the {B / 2**20:g} "
+                           f"MiB payload), one process per GPU, 64 KiB chunks each D2H hipMemcpy -> "
+                           f"shm allreduce -> H2D hipMemcpy (reduce_impl.h:186-228), 1 rep",
+                 "host": host_info()}, extra)
+    t1 = oracle.host_bounce_time(op, dt, n, 0, 1, key + "cpu1", src, dst, reps=1)
+    cpu = {"value": B / GiB / t1, "unit": "GiB/s", "cores": 1, "kind": "port",
+           "sample": f"full workload: 1 PE f32 sum of {B / 2**20:g} MiB, 64 KiB chunks each through "
+                     f"a synchronous D2H hipMemcpy, the (1-member) allreduce and a synchronous H2D "
+                     f"hipMemcpy (reduce_impl.h:186-228, memory.cpp:310-321), 1 rep",
+           "host": host_info()}
+    side = []
+    ns = min(n, (64 << 20) // 4)
+    for p in (2, 4, 8):
+        k = f"{key}cpu{p}"
+        helpers = [subprocess.Popen([sys.executable, "-m", "oracle.bounce_helper", "--me", str(me),
+                                     "--npes", str(p), "--key", k, "--n", str(ns)],
+                                    cwd=str(ROOT), stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                                    text=True) for me in range(1, p)]
+        try:
+            t = oracle.host_bounce_time(op, dt, ns, 0, p, k, src, dst, reps=1)
+            ts = [t] + [float(h.communicate(timeout=120)[0].strip()) for h in helpers]
+            side.append({"pes": p, "value": ns * 4 / GiB / max(ts), "unit": "GiB/s (per PE)",
+                         "cores": p, "sample": f"{ns * 4 >> 20} MiB f32 per PE, {p} processes on "
+                                               f"this one GPU (its PCIe link shared)"})
+        except Exception as ex:
+            side.append({"pes": p, "error": str(ex)})
+        finally:
+            for h in helpers:
+                if h.poll() is None:
+                    h.kill()
+    extra["cpu_baseline_pes"] = side
+    tm = oracle.host_proxy_time(op, dt, n, 1, 2)
+    extra["cpu_baseline_memcpy_only"] = {
+        "value": B / GiB / tm, "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": "round-1 restatement: the same 64 KiB chunking with host memcpys in place of "
+                  "the device copies (optimistic), full workload, best of 2"}
+    n1 = 16 << 20
+    t1 = oracle.host_proxy_time(oracle.OPS["sum"], oracle.DTYPES["int32"], n1, 2, 3)
+    extra["cpu_config1"] = {"value": n1 * 4 / GiB / t1, "unit": "GiB/s", "cores": 2, "kind": "port",
+                            "sample": "BASELINE configs[0]: int32 sum-reduce, 2 PEs (processes), "
+                                      "64 MiB per PE, 64 KiB bounce chunks, host loopback, best of 3"}
+    return cpu, extra
 
 
-def main() -> None:
+def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -232,18 +433,36 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-tripwire", action="store_true")
+    ap.add_argument("--no-full-check", action="store_true")
+    ap.add_argument("--sweep-max-mib", type=int, default=CFG5_MAX_BYTES >> 20)
     ap.add_argument("--nelems", type=int, default=0, help="override: float32 elements per PE")
     ap.add_argument("--no-rccl", action="store_true",
                     help="N>1: skip the RCCL all_reduce comparison on the same payload")
     ap.add_argument("--no-tuning", action="store_true", help="N>1: skip the launch-shape sweep")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args)
+    # Native libraries (gloo, RCCL, HIP) may print to fd 1; keep stdout for the one JSON line by
+    # pointing fd 1 at stderr and writing the line to a duplicate of the original stdout.
+    global _OUT
+    sys.stdout.flush()
+    _OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("bench.py --gpus N>1 must be launched by torch.distributed.run (one rank per GPU)")
+        raise RuntimeError(f"--gpus {args.gpus} but the launcher started {world} ranks")
+    same_device = os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1"
+    n = args.nelems if args.nelems > 0 else (args.mib << 20) // 4
+    B = n * 4
+    sweep_max = min(args.sweep_max_mib << 20, CFG5_MAX_BYTES)
+    if world > 1 and "ISHMEM_SYMMETRIC_SIZE" not in os.environ:
+        # The config-5 sweep holds a 4 GiB source and dest per PE (plus the 128 MiB staging
+        # region): size the symmetric heap for it (288 GB of HBM per GPU).
+        os.environ["ISHMEM_SYMMETRIC_SIZE"] = str(max(2 * B, 2 * sweep_max) + (1 << 30))
     dist = None
     key = f"bench{uuid.uuid4().hex[:10]}"
     if world > 1:
@@ -258,16 +477,14 @@ def main() -> None:
 
     # ISHMEM_BENCH_SAME_DEVICE=1 (development only): every rank on device 0, to measure kernel
     # overheads of the multi-PE path on a one-GPU box.  Never used for reported numbers.
-    device = 0 if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else local_rank
+    device = 0 if same_device else local_rank
     ish.init(rank, world, device, key)
-    n = args.nelems if args.nelems > 0 else (args.mib << 20) // 4
-    B = n * 4
     src = ish.ishmem_malloc(B)
     dst = ish.ishmem_malloc(B)
+    if not (src and dst):
+        raise RuntimeError(f"heap allocation failed: {ish.last_error()}")
     # Synthetic input with an exactly representable sum: x[i] = (i mod 1024) + pe.
-    pattern = (np.arange(n, dtype=np.int64) % 1024).astype(np.float32) + np.float32(rank)
-    hip.upload(src, pattern)
-    del pattern
+    upload_closed_form(hip, src, np.float32, rank, n)
     stream = hip.stream_create()
 
     def barrier():
@@ -287,6 +504,8 @@ def main() -> None:
     barrier()
     if ish.lib().ishmemi_c_error_count():
         raise RuntimeError("device barrier timeouts during warm-up (a PE did not arrive)")
+    hip.memset(dst, 0xFF, B)  # the timed steps must write every word (checked below)
+    barrier()
     ev0, ev1 = hip.Event(), hip.Event()
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -296,41 +515,52 @@ def main() -> None:
     hip.stream_synchronize(stream)
     t1 = time.perf_counter()
     barrier()
-    wall_s = t1 - t0
-    kern_ms = ev0.elapsed_ms(ev1) / args.steps
-    if dist is not None:
-        import torch
-        t = torch.tensor([wall_s, kern_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall_s, kern_ms = float(t[0]), float(t[1])
+    wall_s, kern_ms = max_over_ranks(dist, [t1 - t0, ev0.elapsed_ms(ev1) / args.steps])
     if ish.lib().ishmemi_c_error_count():
         raise RuntimeError("device barrier timeouts during the benchmark")
 
-    # Correctness of the timed buffers (sampled): dest = sum_pe((i mod 1024) + pe).
-    idx = np.random.default_rng(0).integers(0, n, 4096)
-    got = np.array([hip.download(dst + int(i) * 4, 1, np.float32)[0] for i in idx[:256]])
-    exp = (idx[:256] % 1024).astype(np.float32) * world + np.float32(world * (world - 1) / 2)
-    if not np.array_equal(got, exp):
-        raise RuntimeError("benchmark result check failed")
+    # Correctness of the timed buffers: every word of dest on every rank.
+    log("full check of the timed dest")
+    if args.no_full_check:
+        idx = np.random.default_rng(0).integers(0, n, 256)
+        got = np.array([hip.download(dst + int(i) * 4, 1, np.float32)[0] for i in idx])
+        bad = int(np.count_nonzero(got != closed_form("sum", np.float32, world, idx)))
+        checked = {"words": 256, "mode": "sampled"}
+    else:
+        bad = full_check(hip, dst, "sum", np.float32, world, n)
+        checked = {"words": n, "mode": "every word, every rank"}
+    bad = int(max_over_ranks(dist, [float(bad)])[0])
+    if bad:
+        raise RuntimeError(f"benchmark result check failed: {bad} words wrong")
+    checked["wrong"] = 0
 
     ms_per_step = wall_s * 1000.0 / args.steps
     value = world * B / GiB / (ms_per_step / 1000.0)
+    algbw = B / GiB / (ms_per_step / 1000.0)
 
     if world == 1:
         roof = {"bound": "hbm", "achieved": 2 * B / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "traffic": pmc_traffic("copy_1pe", B),
                 "kernel": "fanin_kernel<uint8,OR,vec> (1-PE reduce = copy, 2B per launch)"}
+        t_roof = 2 * B / (HBM_PEAK_GBS * 1e9)
     else:
         link_bytes = 2.0 * (world - 1) / world * B  # RS + AG ingress per PE over p-1 links
         roof = {"bound": "xgmi", "achieved": link_bytes / (kern_ms * 1e-3) / 1e9,
                 "peak": XGMI_LINK_GBS * (world - 1), "unit": "GB/s",
                 "traffic": pmc_traffic(f"allreduce_{world}pe", B),
                 "kernel": "allreduce_kernel<float,SUM,vec> (per-PE xGMI ingress 2(p-1)/p*B)"}
+        t_roof = max((3.0 - 1.0 / world) * B / (HBM_PEAK_GBS * 1e9),
+                     (2.0 * B / world) / (XGMI_LINK_GBS * 1e9))
     roof["frac"] = roof["achieved"] / roof["peak"]
+    algbw_roof = B / GiB / t_roof
+    targets = {"algbw_roofline_GiBps": algbw_roof, "algbw_frac_of_roofline": algbw / algbw_roof}
+    if world == 8:
+        targets["algbw_target_GiBps"] = 400.0  # >= 70 % of 572 GiB/s
+        targets["met"] = algbw >= 400.0
 
     extra = {}
-    log("timed steps done; combine leg")
     if world == 1 and not args.no_combine:
+        log("combine leg")
         # Local combine unit dst = a + b at the same size (3B HBM bytes per launch).
         b2 = ish.ishmem_malloc(B)
         hip.memcpy(b2, src, B)
@@ -349,13 +579,71 @@ def main() -> None:
                             "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("combine2_1pe", B)}
         ish.ishmem_free(b2)
 
-    log("host-memory end-to-end leg")
+    if world > 1 and not args.no_probe:
+        log("xGMI probe")
+        try:
+            probe = xgmi_probe(ish, hip, src, dst, B, world, rank, dist, stream, barrier)
+            extra["xgmi_probe"] = probe
+            # Same accounting as roof["achieved"], against the measured all-peer ingress.
+            roof["peak_measured"] = max(probe["pullall"]["ingress_GBps"], probe["pullall_sc"]["ingress_GBps"])
+            roof["frac_measured"] = roof["achieved"] / roof["peak_measured"]
+        except Exception as ex:
+            extra["xgmi_probe"] = {"error": str(ex)}
+
+    if world > 1 and not args.no_tuning:
+        log("launch-shape sweep")
+        try:
+            extra["xgmi_tuning"] = xgmi_tuning(ish, hip, src, dst, B, world, dist, stream)
+        except Exception as ex:
+            extra["xgmi_tuning"] = {"error": str(ex)}
+
+    cpu = None
+    if not args.no_cpu_baseline and (world > 1 or rank == 0):
+        log("CPU baseline leg (reference host path with its 64 KiB device copies)")
+        try:
+            cpu, more = cpu_baseline_leg(ish, hip, src, dst, n, B, world, rank, dist, key)
+            extra.update(more)
+        except Exception as ex:
+            cpu = {"error": str(ex)}
+
+    ish.ishmem_free(dst)
+    ish.ishmem_free(src)
+
+    if world > 1 and not args.no_tripwire:
+        log("coherence tripwire")
+        from ishmem_amd import selfcheck
+        try:
+            tw = selfcheck.chain_tripwire(ish, hip, rank, world, nmax=16 << 20, iters=8)
+            bad = max_over_ranks(dist, [float(sum(tw["mismatches"])), float(not tw["checked"])])
+            tw["checked"] = bad[0] == 0 and bad[1] == 0
+            tw["mismatches_rank0"] = tw.pop("mismatches")
+            tw["mismatches_all_ranks"] = int(bad[0])
+            extra["tripwire"] = tw
+        except Exception as ex:
+            extra["tripwire"] = {"error": str(ex), "checked": False}
+
+    if world > 1 and not args.no_sweep:
+        log("config-5 sweep")
+        # BASELINE configs[4] (min/max/prod x int32/float64 across the PEs), 4 KiB .. 4 GiB per PE.
+        try:
+            extra["config5_sweep"] = config5_sweep(ish, hip, world, rank, dist, stream, sweep_max)
+        except Exception as ex:
+            extra["config5_sweep"] = {"error": str(ex)}
+
     if not args.no_e2e:
+        # Last: its pipeline streams add hardware queues, which oversubscribe the scheduler when
+        # several ranks share one GPU (same-device rehearsals) and slow every later leg there.
+        log("host-memory end-to-end leg")
         # The path starts and ends in host memory (north star): pinned host source/dest, the
         # library stages H2D -> device reduce -> D2H through HBM as a 3-stream pipeline.
         try:
             hs, hd = hip.host_malloc(B), hip.host_malloc(B)
-            hip.memcpy(hs, src, B)  # same synthetic input as the device-resident run
+            hx = np.ctypeslib.as_array((ctypes.c_float * n).from_address(hs))
+            for lo in range(0, n, 1 << 26):  # same synthetic input as the device-resident run
+                hi = min(n, lo + (1 << 26))
+                hx[lo:hi] = ((np.arange(lo, hi, dtype=np.int64) % 1024) + rank).astype(np.float32)
+            del hx
+
             def step_e2e():
                 return ish.ishmemx_float_sum_reduce_on_stream(hd, hs, n, 0, stream)
             if step_e2e() != 0:  # warm-up (creates the pipeline streams)
@@ -369,15 +657,11 @@ def main() -> None:
             hip.stream_synchronize(stream)
             te = time.perf_counter() - te0
             barrier()
-            if dist is not None:
-                import torch
-                tt = torch.tensor([te], dtype=torch.float64)
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                te = float(tt[0])
+            te = max_over_ranks(dist, [te])[0]
             chk = (ctypes.c_float * 4).from_address(hd + 4 * 1000)
             ok = [float(x) for x in chk] == [float((1000 + i) % 1024 * world + world * (world - 1) / 2) for i in range(4)]
-            extra["e2e_host"] = {"value": world * B / GiB / (te / k), "unit": "GiB/s",
-                                 "ms_per_step": te / k * 1000.0, "steps": k, "checked": ok,
+            extra["e2e_host"] = {"value": world * B / GiB / (te / k), "algbw_GiBps": B / GiB / (te / k),
+                                 "unit": "GiB/s", "ms_per_step": te / k * 1000.0, "steps": k, "checked": ok,
                                  "buffers": "pinned host (hipHostMalloc)",
                                  "pipeline": "H2D | reduce | D2H over 2 staging slots"}
             hip.host_free(hs)
@@ -385,128 +669,43 @@ def main() -> None:
         except Exception as ex:  # reported, never fatal for the main measurement
             extra["e2e_host"] = {"error": str(ex)}
 
-    log("xGMI probe")
-    if world > 1 and not args.no_probe:
-        # Measured link rates (report against the spec AND a measured L).  Plain
-        # pulls of a peer's source through the local combine kernel, no barriers inside:
-        #   pull1   — every rank copies S bytes from rank+1 (ring: each link busy in one direction)
-        #   pullall — every rank folds the sources of all p-1 peers (ingress (p-1)*S per GPU)
-        #   push1   — every rank writes S bytes into rank+1's dest (remote stores)
-        try:
-            S = min(B, 256 << 20)
-            ns = S // 4
-            peers = [(rank + d) % world for d in range(1, world)]
-            probe = {}
-            # pull1 / pullall load nontemporal; the *_sc twins issue the system-coherent (sc0 sc1)
-            # loads the collectives use on peer memory, so each pair shows what that policy costs.
-            cases = (("pull1", [ish.ishmem_ptr(src, peers[0])], dst, 0),
-                     ("pull1_sc", [ish.ishmem_ptr(src, peers[0])], dst, 1),
-                     ("pullall", [ish.ishmem_ptr(src, j) for j in peers], dst, 0),
-                     ("pullall_sc", [ish.ishmem_ptr(src, j) for j in peers], dst, 1),
-                     ("push1", [src], ish.ishmem_ptr(dst, peers[0]), None))
-
-            def launch(srcs, out, pol):
-                if pol is None:
-                    return ish.combine("sum", "float", out, srcs, ns, stream)
-                return ish.pull_probe(out, srcs, S, pol, stream)
-
-            for name, srcs, out, pol in cases:
-                for _ in range(2):
-                    launch(srcs, out, pol)
-                barrier()
-                k = 10
-                e0, e1 = hip.Event(), hip.Event()
-                e0.record(stream)
-                for _ in range(k):
-                    if launch(srcs, out, pol) != 0:
-                        raise RuntimeError(ish.last_error())
-                e1.record(stream)
-                hip.stream_synchronize(stream)
-                ms = e0.elapsed_ms(e1) / k
-                import torch
-                tt = torch.tensor([ms], dtype=torch.float64)
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                ms = float(tt[0])
-                gbs = len(srcs) * S / (ms * 1e-3) / 1e9
-                probe[name] = {"bytes_per_peer": S, "peers": len(srcs), "ms": round(ms, 4),
-                               "ingress_GBps": round(gbs, 1),
-                               "per_link_GBps": round(gbs / len(srcs), 1)}
-            barrier()
-            extra["xgmi_probe"] = probe
-            # Same accounting as roof["achieved"], against the measured all-peer ingress.
-            roof["peak_measured"] = max(probe["pullall"]["ingress_GBps"], probe["pullall_sc"]["ingress_GBps"])
-            roof["frac_measured"] = roof["achieved"] / roof["peak_measured"]
-        except Exception as ex:
-            extra["xgmi_probe"] = {"error": str(ex)}
-
-    log("launch-shape sweep")
-    if world > 1 and not args.no_tuning:
-        try:
-            extra["xgmi_tuning"] = xgmi_tuning(ish, hip, src, dst, B, world, dist, stream)
-        except Exception as ex:
-            extra["xgmi_tuning"] = {"error": str(ex)}
-
-    log("config-5 sweep")
-    if world > 1 and not args.no_sweep:
-        # BASELINE configs[4] (min/max/prod x int32/float64 across the PEs), sizes 4 KiB ..
-        # the payload (1 GiB) per PE (the 4 GiB end of that sweep is left to tools/sweep.py).  Inputs
-        # x_pe[i] = (i mod 1024) + pe; every result is checked against the canonical fold.
-        extra["config5_sweep"] = config5_sweep(ish, hip, src, dst, B, world, rank, dist, stream)
-
-    log("CPU baseline leg")
-    cpu = None
-    if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        import oracle  # CPU baseline leg only: the reference's host-proxy reduce, restated
-        reps = 3
-        t_cpu = oracle.host_proxy_time(oracle.OPS["sum"], oracle.DTYPES["float"], n, 1, reps)
-        cpu = {"value": B / GiB / t_cpu, "unit": "GiB/s", "cores": 1, "kind": "port",
-               "sample": f"full workload: 1 PE f32 sum-reduce of {B / 2**20:g} MiB through 64 KiB host "
-                         f"bounce chunks (reduce_impl.h:186-228), best of {reps}"}
-        # BASELINE configs[0]: int32 sum, 2 PEs, host loopback through the proxy path (no GPU):
-        # two processes exchanging 64 KiB bounce chunks over shared memory.
-        n1 = 16 << 20
-        t1 = oracle.host_proxy_time(oracle.OPS["sum"], oracle.DTYPES["int32"], n1, 2, 3)
-        extra["cpu_config1"] = {"value": n1 * 4 / GiB / t1, "unit": "GiB/s", "cores": 2,
-                                "kind": "port", "sample": "int32 sum-reduce, 2 PEs (processes), "
-                                "64 MiB per PE, 64 KiB bounce chunks, best of 3"}
-
-    ish.ishmem_free(dst)
-    ish.ishmem_free(src)
     hip.stream_destroy(stream)
     ish.ishmem_finalize()
     line = None
     if rank == 0:
         line = {
-            "metric": "GiB/s device-resident float32 sum-reduce at 1/2/4/8 PEs vs HBM+xGMI roofline",
-            "value": value, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC, "value": value, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "value_definition": "whole job: N PEs x B payload bytes / time per step (N*B/t)",
+            "algbw_GiBps": algbw,
+            "algbw_definition": "per PE: B / time per step (test/include/ishmem_tester.h:1553-1555)",
             "config": {"workload": f"float32 sum-reduce, {B / 2**20:g} MiB per PE, {world} PE(s), "
                                    f"symmetric-heap device buffers", "nreduce": n,
                        "bytes_per_pe": B, "pes": world,
                        "parallelism": "1 PE self-reduce" if world == 1 else f"direct RS+AG over {world} PEs"},
-            "kernel_ms": kern_ms,
-            **({"dev_same_device": True} if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else {}), "roofline": roof, "cpu_baseline": cpu, **extra,
+            "kernel_ms": kern_ms, "checked": checked, "targets": targets,
+            **({"dev_same_device": True} if same_device else {}), "roofline": roof,
+            "cpu_baseline": cpu, **extra,
         }
-    if world > 1 and not args.no_rccl and os.environ.get("ISHMEM_BENCH_SAME_DEVICE") != "1":
+    if world > 1 and not args.no_rccl and not same_device:
         log("RCCL comparison leg")
         rccl = rccl_allreduce(dist, device, n, B, world, args.steps, line)
         if line is not None:
             line["rccl_allreduce"] = rccl
     if line is not None:
-        print(json.dumps(line), flush=True)
+        emit(line)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
     try:
-        main()
+        sys.exit(main())
     except Exception as exc:  # always leave one JSON line for the driver, with the reason
         if int(os.environ.get("RANK", "0")) == 0:
-            print(json.dumps({
-                "metric": "GiB/s device-resident float32 sum-reduce at 1/2/4/8 PEs vs HBM+xGMI roofline",
-                "value": None, "unit": "GiB/s", "n_gpus": int(os.environ.get("WORLD_SIZE", "1")),
-                "higher_is_better": True, "error": f"{type(exc).__name__}: {exc}"}))
-        sys.stdout.flush()
+            emit({"metric": METRIC, "value": None, "unit": "GiB/s",
+                  "n_gpus": int(os.environ.get("WORLD_SIZE", "1")),
+                  "higher_is_better": True, "error": f"{type(exc).__name__}: {exc}"})
         raise

@@ -48,6 +48,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_host_proxy_reduce.argtypes = [i, i, ctypes.POINTER(vp), ctypes.POINTER(vp), i, sz]
         L.oracle_host_proxy_time.argtypes = [i, i, sz, i, i]
         L.oracle_host_proxy_time.restype = ctypes.c_double
+        L.oracle_host_bounce_time.argtypes = [i, i, sz, i, i, ctypes.c_char_p, vp, vp, vp, i]
+        L.oracle_host_bounce_time.restype = ctypes.c_double
         L.oracle_pattern_source.argtypes = [i, i, i, sz, vp]
         L.oracle_pattern_check.argtypes = [i, i, i, i, sz, vp]
         L.oracle_fill_random.argtypes = [i, ctypes.c_uint64, ctypes.c_double, ctypes.c_double, sz, vp]
@@ -89,6 +91,34 @@ def host_proxy_reduce(op: int, dt: int, srcs: list[np.ndarray]) -> list[np.ndarr
 def host_proxy_time(op: int, dt: int, n: int, npes: int, reps: int = 3) -> float:
     """Best wall seconds of the multi-process host-proxy restatement (CPU baseline)."""
     return float(lib().oracle_host_proxy_time(op, dt, n, npes, reps))
+
+
+def hip_memcpy_fn() -> int:
+    """Address of hipMemcpy in the HIP runtime (the copy the reference's host path makes with
+    Level Zero, src/memory.cpp:310-321), for oracle_host_bounce_time."""
+    for cand in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+        try:
+            h = ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
+            return ctypes.cast(h.hipMemcpy, ctypes.c_void_p).value
+        except OSError:
+            continue
+    raise OSError("libamdhip64.so not found")
+
+
+COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
+
+
+def host_bounce_time(op: int, dt: int, n: int, me: int, npes: int, key: str, dev_src: int,
+                     dev_dst: int, reps: int = 1, copy_fn=None) -> float:
+    """This member's best wall seconds of the reference's host path with its real synchronous
+    64 KiB device<->host copies (oracle_host_bounce_time); every member calls it.  copy_fn
+    defaults to hipMemcpy (a COPY_FN callback may stand in for it in CPU tests)."""
+    fn = hip_memcpy_fn() if copy_fn is None else ctypes.cast(copy_fn, ctypes.c_void_p).value
+    t = float(lib().oracle_host_bounce_time(op, dt, n, me, npes, key.encode(), dev_src, dev_dst,
+                                            fn, reps))
+    if t < 0:
+        raise RuntimeError(f"oracle_host_bounce_time failed ({t})")
+    return t
 
 
 def pattern_source(family: int, dt: int, pe: int, nelems: int) -> np.ndarray:

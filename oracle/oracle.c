@@ -219,6 +219,123 @@ double oracle_host_proxy_time(int op, int dt, size_t n, int npes, int reps)
 }
 
 /* ---------------------------------------------------------------------------------------------
+ * The reference's host path INCLUDING its device copies, for the CPU baseline: each PE is a
+ * process of its own (the caller), its source / dest are device memory, and every 64 KiB chunk
+ * goes through a synchronous device->host copy into this PE's bounce buffer
+ * (ishmemi_copy(team.source, src), src/collectives/reduce_impl.h:196 -> src/memory.cpp:310-321,
+ * a synchronous immediate command list), the MPI shared-memory allreduce of the p bounce buffers
+ * (runtime_mpi.cpp:802-812: reduce-scatter + all-gather through shared memory, restated as
+ * above), and a synchronous host->device copy back (:218).  The copies go through `copy_fn`,
+ * which the caller binds to hipMemcpy (kind 2 = device->host, 1 = host->device), so this file
+ * stays free of any GPU header.  The p processes meet in a POSIX shared-memory segment named by
+ * `key`; member 0 creates it.  Returns this member's best seconds over `reps`; < 0 on failure.
+ * ------------------------------------------------------------------------------------------- */
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <sys/stat.h>
+
+struct bounce_ctl {
+    int magic, count, gen, pad;
+};
+#define BOUNCE_MAGIC 0x1B0C0E5
+
+/* Shared-memory spin barrier (what an MPI shared-memory transport polls), bounded: returns
+ * nonzero if the other members do not arrive within 60 s (a member that died). */
+static int bounce_barrier(struct bounce_ctl *c, int npes)
+{
+    const int g = __atomic_load_n(&c->gen, __ATOMIC_ACQUIRE);
+    if (__atomic_fetch_add(&c->count, 1, __ATOMIC_ACQ_REL) == npes - 1) {
+        __atomic_store_n(&c->count, 0, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&c->gen, 1, __ATOMIC_RELEASE);
+        return 0;
+    }
+    const double t0 = wall();
+    for (unsigned it = 0; __atomic_load_n(&c->gen, __ATOMIC_ACQUIRE) == g; ++it)
+        if ((it & 1023) == 1023 && wall() - t0 > 60.0) return 1;
+    return 0;
+}
+
+double oracle_host_bounce_time(int op, int dt, size_t n, int me, int npes, const char *key,
+                               const void *dev_src, void *dev_dst, oracle_copy_fn copy_fn,
+                               int reps)
+{
+    if (!oracle_valid(op, dt) || npes < 1 || me < 0 || me >= npes || reps < 1 || !copy_fn || !key)
+        return -1.0;
+    const size_t es = oracle_dtype_size(dt);
+    const size_t chunk = REDUCE_BUFFER_SIZE / es;
+    const size_t total = 4096 + (size_t) npes * REDUCE_BUFFER_SIZE + REDUCE_BUFFER_SIZE;
+    char name[256];
+    snprintf(name, sizeof(name), "/ishmem_oracle_bounce_%s", key);
+    int fd = -1;
+    const double t_attach = wall();
+    if (me == 0) {
+        shm_unlink(name);
+        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0 || ftruncate(fd, (off_t) total) != 0) return -2.0;
+    } else {
+        while ((fd = shm_open(name, O_RDWR, 0600)) < 0) {
+            if (wall() - t_attach > 60.0) return -3.0;
+            usleep(1000);
+        }
+        struct stat st;
+        while (fstat(fd, &st) == 0 && (size_t) st.st_size < total) {
+            if (wall() - t_attach > 60.0) return -3.0;
+            usleep(1000);
+        }
+    }
+    char *base = mmap(NULL, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (base == MAP_FAILED) return -4.0;
+    struct bounce_ctl *ctl = (struct bounce_ctl *) base;
+    if (me == 0) {
+        ctl->count = 0;
+        ctl->gen = 0;
+        __atomic_store_n(&ctl->magic, BOUNCE_MAGIC, __ATOMIC_RELEASE);
+    } else {
+        while (__atomic_load_n(&ctl->magic, __ATOMIC_ACQUIRE) != BOUNCE_MAGIC) {
+            if (wall() - t_attach > 60.0) {
+                munmap(base, total);
+                return -3.0;
+            }
+            usleep(1000);
+        }
+    }
+    char *bsrc = base + 4096;
+    char *bres = bsrc + (size_t) npes * REDUCE_BUFFER_SIZE;
+    char *mine = bsrc + (size_t) me * REDUCE_BUFFER_SIZE;
+    double best = 1e30;
+    int failed = 0;
+    for (int r = 0; r < reps && !failed; ++r) {
+        failed |= bounce_barrier(ctl, npes);
+        const double t0 = wall();
+        for (size_t off = 0; off < n && !failed; off += chunk) {
+            const size_t m = (n - off < chunk) ? n - off : chunk;
+            failed |= copy_fn(mine, (const char *) dev_src + off * es, m * es, 2) != 0;
+            failed |= bounce_barrier(ctl, npes);
+            const size_t part = (m + (size_t) npes - 1) / (size_t) npes;
+            const size_t lo = (size_t) me * part < m ? (size_t) me * part : m;
+            const size_t hi = lo + part < m ? lo + part : m;
+            if (hi > lo) {
+                memcpy(bres + lo * es, bsrc + lo * es, (hi - lo) * es);
+                for (int pe = 1; pe < npes; ++pe)
+                    oracle_combine(op, dt, bres + lo * es,
+                                   bsrc + (size_t) pe * REDUCE_BUFFER_SIZE + lo * es, hi - lo);
+            }
+            failed |= bounce_barrier(ctl, npes);
+            failed |= copy_fn((char *) dev_dst + off * es, bres, m * es, 1) != 0;
+            failed |= bounce_barrier(ctl, npes);
+        }
+        const double t1 = wall();
+        if (t1 - t0 < best) best = t1 - t0;
+    }
+    if (!failed) failed |= bounce_barrier(ctl, npes);
+    if (me == 0) shm_unlink(name);
+    munmap(base, total);
+    return failed ? -5.0 : best;
+}
+
+/* ---------------------------------------------------------------------------------------------
  * Reference known-answer patterns.
  * ------------------------------------------------------------------------------------------- */
 

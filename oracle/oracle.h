@@ -56,6 +56,17 @@ int oracle_host_proxy_reduce(int op, int dt, const void *const *srcs, void *cons
  * `reps` repetitions of one reduce of n elements; -1 on failure. */
 double oracle_host_proxy_time(int op, int dt, size_t n, int npes, int reps);
 
+/* The same host path with its real device copies (CPU baseline of bench.py): called by each of
+ * `npes` processes (member `me`, rendezvous by `key`) on its own DEVICE source / dest; every
+ * 64 KiB chunk is copied device->host with copy_fn(dst, src, bytes, 2), all-reduced through
+ * shared memory, and copied host->device with copy_fn(dst, src, bytes, 1) — both synchronous,
+ * like ishmemi_copy (src/memory.cpp:310-321).  copy_fn is hipMemcpy, bound by the caller.
+ * Returns this member's best wall seconds over `reps`; < 0 on failure. */
+typedef int (*oracle_copy_fn)(void *dst, const void *src, size_t bytes, int kind);
+double oracle_host_bounce_time(int op, int dt, size_t n, int me, int npes, const char *key,
+                               const void *dev_src, void *dev_dst, oracle_copy_fn copy_fn,
+                               int reps);
+
 /* Reference known-answer patterns (test/unit/reduce_*.cpp).  `out` receives nelems elements
  * (nelems * size bytes, built from the 64-bit word pattern exactly like the tester). */
 int oracle_pattern_source(int family, int dt, int pe, size_t nelems, void *out);

@@ -33,15 +33,10 @@ for s in $STEPS; do
     single) run pytest_single 900 python -m pytest tests/test_gpu_single.py -m gpu -x -q -p no:cacheprovider ;;
     multi)  run pytest_multi 1200 python -m pytest tests/test_gpu_multi.py -m gpu -x -q -p no:cacheprovider ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
-    local2) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-256} run bench_local2 600 python -m torch.distributed.run \
-                --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 \
-                --steps 10 --warmup 3 --mib ${MIB:-1024} ;;
-    local4) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-128} run bench_local4 600 python -m torch.distributed.run \
-                --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 4 \
-                --steps 10 --warmup 3 --mib ${MIB:-512} ;;
-    local8) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-16} ISHMEM_SYMMETRIC_SIZE=1G run bench_local8 600 \
-                python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
-                --master-port 29520 bench.py --gpus 8 --steps 5 --warmup 2 --mib ${MIB:-128} ;;
+    local2|local4|local8)  # N-rank rehearsal on the one GPU (self-launched ranks, same device)
+            np_=${s#local}
+            ISHMEM_BENCH_SAME_DEVICE=1 run bench_$s 900 python bench.py --gpus $np_ --steps 10 --warmup 3 \
+                --mib ${MIB:-1024} --sweep-max-mib ${SWEEP_MIB:-4096} ;;
     sweep1) run sweep1 300 python tools/sweep.py --max-mib 1024 ;;
     sweep2) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-256} run sweep2 600 python -m torch.distributed.run \
                 --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 tools/sweep.py --max-mib 256 ;;

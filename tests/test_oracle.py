@@ -136,3 +136,49 @@ def test_collect_check_is_concatenation_of_sources():
     assert np.array_equal(chk, np.concatenate(src))
     w = oracle.collect_pattern_source(1, 4, 8).view(np.uint64)
     assert int(w[2]) == (4 << 48) + (0x81 << 40) + (0xff << 32) + 2  # fcollect.cpp:54-55
+
+
+def _bounce_member(me, npes, key, n, q):
+    import ctypes
+
+    import numpy as np
+
+    import oracle
+    src = oracle.fill_random(oracle.DTYPES["int32"], 0xB0 + me, n)
+    dst = np.zeros(n, np.int32)
+    calls = []
+
+    def copy(d, s, nb, kind):  # stands in for hipMemcpy: host arrays play the device buffers
+        calls.append(kind)
+        ctypes.memmove(d, s, nb)
+        return 0
+    fn = oracle.COPY_FN(copy)
+    t = oracle.host_bounce_time(oracle.OPS["sum"], oracle.DTYPES["int32"], n, me, npes, key,
+                                src.ctypes.data, dst.ctypes.data, reps=2, copy_fn=fn)
+    q.put((me, t, dst, calls.count(2), calls.count(1)))
+
+
+@pytest.mark.parametrize("npes", [1, 3])
+def test_host_bounce_restatement_reduces_through_64KiB_device_copies(npes):
+    # oracle_host_bounce_time (the CPU baseline with the reference's synchronous 64 KiB copies,
+    # reduce_impl.h:186-228): every member ends with the rank-order fold, and makes exactly one
+    # device->host and one host->device copy per chunk and repetition.
+    import multiprocessing as mp
+    import uuid
+    n = 100_003
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    key = f"tb{uuid.uuid4().hex[:8]}"
+    ps = [ctx.Process(target=_bounce_member, args=(me, npes, key, n, q)) for me in range(npes)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(npes)]
+    for p in ps:
+        p.join(timeout=30)
+    srcs = [oracle.fill_random(oracle.DTYPES["int32"], 0xB0 + j, n) for j in range(npes)]
+    want = oracle.reduce_fold(oracle.OPS["sum"], oracle.DTYPES["int32"], srcs, 0)
+    chunks = -(-n * 4 // oracle.REDUCE_BUFFER_SIZE)
+    for me, t, dst, d2h, h2d in res:
+        assert t > 0
+        assert np.array_equal(dst, want), f"member {me}"
+        assert d2h == 2 * chunks and h2d == 2 * chunks
