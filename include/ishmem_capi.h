@@ -101,6 +101,11 @@ void ishmemi_c_team_destroy(int team);
 int ishmemi_c_barrier_all(void);
 int ishmemi_c_sync_all(void);
 int ishmemi_c_team_sync(int team);
+/* Recovery after a device-side timeout (no reference counterpart: the reference aborts the job,
+ * src/proxy.cpp:79-84).  Collective over ALL PEs, called with no collective in flight: the PEs
+ * agree on the newest epoch of every team over the bootstrap, so later collectives of a team whose
+ * members fell out of step work again; pending device error words are cleared. */
+int ishmemi_c_resync(void);
 
 /* ---- THE HOT PATH ----------------------------------------------------------------------------
  * ishmemi_c_reduce: blocking reduction over a team.  Replaces every

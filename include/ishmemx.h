@@ -4,8 +4,9 @@
  *   sycl::event ishmemx_<TYPENAME>_<op>_reduce_on_queue([team,] dest, source, nreduce, int *ret,
  *                                                       sycl::queue &q, deps = {})
  * (src/ishmemx.h:1172-1803, src/collectives/reduce_impl.h:444-474) becomes the HIP-stream
- * variant below: enqueue on `stream`, return immediately (0 = enqueued), the kernel stores 0 into
- * *ret (device-visible int, may be nullptr) when the collective completed successfully.
+ * variant below: enqueue on `stream`, return immediately (0 = enqueued); *ret (device-visible
+ * int, may be nullptr) is zeroed in stream order at the call's start and set nonzero by any of the
+ * call's launches that fails, so it reads 0 after completion exactly when the call succeeded.
  * Dependencies are expressed by stream order / hipStreamWaitEvent instead of `deps`.
  */
 #ifndef ISHMEM_AMD_ISHMEMX_H
@@ -14,6 +15,10 @@
 #include "ishmem.h"
 
 #define ISHMEMX_TEAM_NODE ISHMEMI_C_TEAM_NODE /* src/ishmemx.h:11 */
+
+/* After a device-side timeout, all PEs agree on the teams' epochs again (collective over all PEs;
+ * no reference counterpart — the reference aborts, src/proxy.cpp:79-84). */
+inline int ishmemx_resync(void) { return ishmemi_c_resync(); }
 
 typedef struct ihipStream_t *hipStream_t; /* identical to HIP's own typedef */
 

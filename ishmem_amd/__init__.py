@@ -156,6 +156,11 @@ def ishmem_barrier_all() -> int:
     return _L.ishmemi_c_barrier_all()
 
 
+def resync() -> int:
+    """After a device-side timeout: all PEs agree on every team's epoch again (collective)."""
+    return _L.ishmemi_c_resync()
+
+
 def ishmem_sync_all() -> int:
     return _L.ishmemi_c_sync_all()
 

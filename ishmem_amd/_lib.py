@@ -35,6 +35,7 @@ PROTOTYPES = [
     ("ishmemi_c_barrier_all", _i, []),
     ("ishmemi_c_sync_all", _i, []),
     ("ishmemi_c_team_sync", _i, [_i]),
+    ("ishmemi_c_resync", _i, []),
     ("ishmemi_c_reduce", _i, [_i, _i, _i, _vp, _vp, _sz]),
     ("ishmemi_c_reduce_on_stream", _i, [_i, _i, _i, _vp, _vp, _sz, _vp, _vp]),
     ("ishmemi_c_combine", _i, [_i, _i, _vp, ctypes.POINTER(_vp), _i, _sz, _vp]),

@@ -1286,6 +1286,53 @@ int ishmemi_c_barrier_all(void)
     return ishmemi_c_team_sync(ISHMEMI_C_TEAM_WORLD);
 }
 
+int ishmemi_c_resync(void)
+{
+    // After a device-side timeout the members of a team disagree on its epoch (a PE that timed
+    // out advanced, a PE that never arrived did not), so every later collective of the team would
+    // time out too.  The reference aborts the job instead (src/proxy.cpp:79-84).  Here every PE,
+    // with no collective of its own in flight, agrees on the wrap-safe maximum of every team's
+    // epochs (host and device-API launches) over the bootstrap; every flag row and ring granule
+    // then holds an epoch <= the new one, so the next launch starts clean on every member.
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.initialized) return fail("resync: not initialized");
+    HIP_TRY(hipDeviceSynchronize());
+    struct Epochs {
+        uint32_t host[kMaxTeams], dev[kMaxTeams];
+    } mine{}, all[kMaxPes];
+    uint32_t words[kMaxTeams * kEpWords];
+    HIP_TRY(hipMemcpy(words, s.kern_ep, sizeof(words), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(mine.dev, s.dev_epochs, sizeof(mine.dev), hipMemcpyDeviceToHost));
+    for (int t = 0; t < kMaxTeams; ++t) mine.host[t] = words[t * kEpWords + kEpEpoch];
+    if (s.npes > 1) {
+        std::string err;
+        if (s.boot.allgather(&mine, all, sizeof(Epochs), err)) return fail("resync: " + err);
+    } else {
+        all[0] = mine;
+    }
+    auto newest = [](uint32_t a, uint32_t b) { return (int32_t) (b - a) > 0 ? b : a; };
+    for (int t = 0; t < kMaxTeams; ++t) {
+        uint32_t h = all[0].host[t], d = all[0].dev[t];
+        for (int j = 1; j < s.npes; ++j) {
+            h = newest(h, all[j].host[t]);
+            d = newest(d, all[j].dev[t]);
+        }
+        for (int k = 0; k < kEpWords; ++k) words[t * kEpWords + k] = 0;
+        words[t * kEpWords + kEpEpoch] = h;
+        mine.dev[t] = d;
+    }
+    HIP_TRY(hipMemcpy(s.kern_ep, words, sizeof(words), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s.dev_epochs, mine.dev, sizeof(mine.dev), hipMemcpyHostToDevice));
+    for (int t = 0; t <= kMaxTeams; ++t) __atomic_store_n(&s.err_host[t], 0u, __ATOMIC_RELEASE);
+    HIP_TRY(hipDeviceSynchronize());
+    if (s.npes > 1) {
+        std::string err;
+        if (s.boot.barrier(err)) return fail("resync: " + err);
+    }
+    return 0;
+}
+
 int ishmemi_c_reduce(int team, int op, int dtype, void *dest, const void *source, size_t nreduce)
 {
     return reduce_impl(team, op, dtype, dest, source, nreduce, nullptr, 0, true);

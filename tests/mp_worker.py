@@ -93,8 +93,8 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
         if "timeout" in scenarios:
             # Failure detection: PE 0 enters collectives PE 1 never joins.  Every device-side
             # spin is bounded, so the call returns nonzero with a diagnostic instead of hanging
-            # (LL granule path and three-barrier path).  The team's epochs now disagree, so the
-            # job ends here, as after any collective error.
+            # (LL granule path and three-barrier path).  The team's epochs now disagree until
+            # every PE calls resync (below), after which collectives work again.
             ish.set_param("timeout_ms", 300)
             s_b, d_b = heap(1 << 20, DT["float"]), heap(1 << 20, DT["float"])
             ret = ish.ishmem_malloc(4)
@@ -123,6 +123,19 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                     if int(hip.download(ret, 1, np.int32)[0]) == 0 and r == 0:
                         fails.append(f"pe0 on_stream n={n} host={host}: *ret is 0 after a timed-out launch")
                 hip.stream_destroy(st)
+            # Recovery: both PEs resynchronise the team epochs, then collectives work again on
+            # the three-phase and the granule paths (and the error words are clear).
+            ish.set_param("timeout_ms", 20000)
+            if ish.resync() != 0:
+                fails.append(f"pe{pe} resync failed: {ish.last_error()}")
+            for n in (1 << 20, 100):
+                ins = [oracle.fill_random(DT["float"], 0x5E + j, n) for j in range(npes)]
+                hip.upload(s_b, ins[pe])
+                r = ish.ishmem_float_sum_reduce(d_b, s_b, n)
+                if r:
+                    fails.append(f"pe{pe} after resync n={n}: rc={r} {ish.last_error()}")
+                else:
+                    check(f"after resync n={n}", OPS["sum"], DT["float"], ins, hip.download(d_b, n, np.float32))
             ish.ishmem_finalize()
             q.put((pe, fails))
             return
