@@ -613,7 +613,7 @@ def main() -> int:
         log("coherence tripwire")
         from ishmem_amd import selfcheck
         try:
-            tw = selfcheck.chain_tripwire(ish, hip, rank, world, nmax=16 << 20, iters=8)
+            tw = selfcheck.chain_tripwire(ish, hip, rank, world, nmax=16 << 20, iters=8, stream=stream)
             bad = max_over_ranks(dist, [float(sum(tw["mismatches"])), float(not tw["checked"])])
             tw["checked"] = bad[0] == 0 and bad[1] == 0
             tw["mismatches_rank0"] = tw.pop("mismatches")

@@ -34,10 +34,24 @@ constexpr int kFaninBlock = 64;  // local combine: one wave, one 16-B item per t
 // arrays (> 32 GiB of 16-B items) take the kernel's grid-stride loop.
 constexpr int kFaninMaxGrid = (int) ((1ull << 31) / kFaninBlock);
 
-// Per-team launch words (device memory, uncached, kEpWords u32 per team; `ep_ctr` in the
-// argument structs points at the team's first word).  All are zero between launches except
-// kEpEpoch; the launch's last workgroup resets the others.
-constexpr int kEpWords = 16;
+// Per-team launch words (device memory, kEpTeamWords u32 per team; `ep_ctr` in the argument
+// structs points at the team's first word).  Line 0 (16 words) holds the kEp* words below; all
+// are zero between launches except kEpEpoch; the launch's last workgroup resets the others.
+// Words read or updated by every workgroup of a launch are spread over 64-B lines of their own,
+// so hundreds of workgroups never queue on one line (MI355X_MICROARCH.md: a counter with 255
+// arrivals costs ~3.3 us; sharded per XCD it is ~8x less contended):
+//   lines kEpRepLine .. +63  - replicas of the epoch (workgroup b reads replica b mod 64);
+//   lines kEpShardLine .. +7 - the "finished" count sharded by blockIdx mod 8, line
+//                              kEpTopLine counts the shards that completed.
+constexpr int kEpWords = 16;  // words of line 0
+constexpr int kLineWords = 16;
+constexpr int kEpReplicas = 64;
+constexpr int kEpRepLine = 1, kEpShardLine = kEpRepLine + kEpReplicas, kEpShards = 8;
+constexpr int kEpTopLine = kEpShardLine + kEpShards;
+//   lines kEpClaimLine ..    - one claim word per reduce-scatter segment (kMaxBlocks), holding
+//                              the epoch of the launch that claimed it (never reset).
+constexpr int kEpClaimLine = kEpTopLine + 1;
+constexpr int kEpTeamWords = kEpClaimLine * kLineWords + kMaxBlocks;
 constexpr int kEpEpoch = 0;    // epoch of the team's last launch
 constexpr int kEpDone = 1;     // workgroups of this launch that have finished
 constexpr int kEpRsHead = 2;   // next reduce-scatter segment (scan: phase-1 piece) to grab
@@ -62,8 +76,9 @@ struct ReduceArgs {
     uint64_t seg_items;      // items per reduce-scatter segment (a multiple of kBlock*kUnroll)
     uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
     int oneshot;  // 1: every member folds the WHOLE array (no hand-off, no all-gather)
-    uint32_t *ep_ctr;  // team's launch words (kEpWords, see kEp*)
+    uint32_t *ep_ctr;  // team's launch words (kEpTeamWords, see kEp*)
     int p, me;
+    uint64_t *trace;     // development phase timestamps (set_param "trace_buffer"), normally null
 };
 
 // Small-message ("LL") path: 8-byte granules {4 data bytes | 32-bit epoch} pushed into every
@@ -81,7 +96,7 @@ struct LLArgs {
     int *ret;
     uint64_t nbytes;
     uint64_t timeout_ticks;
-    uint32_t *ep_ctr;  // team's launch words (kEpWords, see kEp*)
+    uint32_t *ep_ctr;  // team's launch words (kEpTeamWords, see kEp*)
     int p, me;
 };
 hipError_t launch_ll(int op, int dt, const LLArgs &a, hipStream_t s);
@@ -98,7 +113,7 @@ struct CollectArgs {
     uint32_t *err;
     int *ret;
     uint64_t timeout_ticks;
-    uint32_t *ep_ctr;  // team's launch words (kEpWords, see kEp*)
+    uint32_t *ep_ctr;  // team's launch words (kEpTeamWords, see kEp*)
     int p, me;
     int unit;  // bytes per item: 16, 4 or 1 (largest dividing every address and length)
 };
@@ -115,7 +130,7 @@ struct ScanArgs {
     int *ret;
     uint64_t nelems, items_per_chunk;
     uint64_t timeout_ticks;
-    uint32_t *ep_ctr;  // team's launch words (kEpWords, see kEp*)
+    uint32_t *ep_ctr;  // team's launch words (kEpTeamWords, see kEp*)
     int p, me;
     int inclusive;
 };

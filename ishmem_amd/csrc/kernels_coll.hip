@@ -147,8 +147,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
                 scan_item_fold<T, T, 0>(a, base, row, (uint32_t) ((el - nI * E) * sizeof(T)), p, me, true);
             }
             drain_block();
-            if (tid == 0 && __hip_atomic_fetch_add(a.ep_ctr + kEpP1Done, 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT) == npieces - 1) {
+            if (tid == kSignalLane && __hip_atomic_fetch_add(a.ep_ctr + kEpP1Done, 1u, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT) == npieces - 1) {
                 release_system();
                 push_flag(a, kPhaseMid, 0, ep, true);
             }

@@ -155,23 +155,36 @@ __device__ __forceinline__ uint32_t kernel_epoch(const A &a)
 {
     __shared__ uint32_t s_ep;
     if (threadIdx.x == 0) {
-        const uint32_t e =
-            __hip_atomic_load(a.ep_ctr + kEpEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+        const uint32_t *rep = a.ep_ctr + (kEpRepLine + blockIdx.x % kEpReplicas) * kLineWords;
+        const uint32_t e = __hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
         s_ep = e == 0 ? 2u : e;
     }
     __syncthreads();
-    return s_ep;
+    return __builtin_amdgcn_readfirstlane(s_ep);
 }
 
+// One whole wave: the team's epoch and its 64 replicas (one per lane, each on its own line).
+template <typename A>
+__device__ __forceinline__ void publish_epoch_wave(const A &a, uint32_t ep)
+{
+    const int r = threadIdx.x & 63;
+    __hip_atomic_store(a.ep_ctr + (kEpRepLine + r) * kLineWords, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (r == 0) __hip_atomic_store(a.ep_ctr + kEpEpoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// End of the small kernels (LL, team sync; grids of a few workgroups): the last workgroup
+// publishes the epoch.  All threads call.
 template <typename A>
 __device__ __forceinline__ void kernel_epoch_done(const A &a, uint32_t ep)
 {
-    if (threadIdx.x == 0) {
-        if (__hip_atomic_fetch_add(a.ep_ctr + kEpDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
-            gridDim.x - 1) {
-            __hip_atomic_store(a.ep_ctr + kEpDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(a.ep_ctr + kEpEpoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+    __shared__ int s_last;
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(a.ep_ctr + kEpDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 gridDim.x - 1;
+    __syncthreads();
+    if (s_last && threadIdx.x < 64) {
+        if (threadIdx.x == 0) __hip_atomic_store(a.ep_ctr + kEpDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        publish_epoch_wave(a, ep);
     }
 }
 
@@ -224,16 +237,21 @@ __device__ __forceinline__ void launch_fail(const A &a, int phase)
 // (sc0 sc1) load, which neither L1 nor a stale L2 line can satisfy; the wavefront fence only
 // keeps the compiler from hoisting those loads above the poll (cdna_hip_programming.md
 // Guideline 16).
+// Returns 0 when the flags are there, 1 on timeout / launch failure, 2 when `patience` ticks
+// (0 = unlimited) passed first — the caller may then do something else and wait again.
 template <typename A>
-__device__ bool block_wait(const A &a, uint32_t ep, int phase, int slot, int who)
+__device__ int block_wait_ex(const A &a, uint32_t ep, int phase, int slot, int who, uint64_t patience)
 {
     __shared__ int s_ok;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         bool done = lane >= a.p || (who == -1 && lane == a.me) || (who >= 0 && lane != who);
         const uint32_t *row = flag_slot(a.my_flags, phase, slot);
-        bool ok = true;
+        int st = 0;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        // One poll in flight, then a back-off once the wait is long: hundreds of waiting
+        // workgroups polling uncached memory back to back take HBM bandwidth from the workgroups
+        // still streaming (two polls in flight, tried, slowed 1 GiB at 8 PEs on one GPU by 60 %).
         for (uint32_t it = 0;; ++it) {
             if (!done) {
                 const uint32_t v = __hip_atomic_load(row + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -241,37 +259,80 @@ __device__ bool block_wait(const A &a, uint32_t ep, int phase, int slot, int who
             }
             if (__all(done)) break;
             if ((it & 15) == 15) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+                const uint64_t waited = __builtin_amdgcn_s_memrealtime() - t0;
+                if (waited > a.timeout_ticks) {
                     if (lane == 0) launch_fail(a, phase);
-                    ok = false;
+                    st = 1;
+                    break;
+                }
+                if (patience && waited > patience) {
+                    st = 2;
                     break;
                 }
                 if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(
                         a.ep_ctr + kEpFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0) {
-                    ok = false;
+                    st = 1;
                     break;
                 }
             }
-            __builtin_amdgcn_s_sleep(1);
+            if (it < 32) __builtin_amdgcn_s_sleep(1);
+            else __builtin_amdgcn_s_sleep(8);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane == 0) s_ok = ok;
+        if (lane == 0) s_ok = st;
     }
     __syncthreads();
-    return s_ok != 0;
+    return __builtin_amdgcn_readfirstlane(s_ok);
 }
 
-// All threads call: one returning device-scope add on a launch word, broadcast to the block
-// (the dequeue primitive of MI355X_MICROARCH.md's price list).
 template <typename A>
-__device__ __forceinline__ uint32_t block_grab(const A &a, int word)
+__device__ bool block_wait(const A &a, uint32_t ep, int phase, int slot, int who)
+{
+    return block_wait_ex(a, ep, phase, slot, who, 0) == 0;
+}
+
+// Work grabbing with one grab in flight (the dequeue primitive of MI355X_MICROARCH.md's price
+// list: a returning device-scope add on a launch word, ~1 us under load).  grab_issue: lane 0
+// issues the add and does not wait; grab_take (all threads) waits for it and broadcasts the
+// value.  Issued before an item's loads, the add's latency hides behind them.
+// Lane roles inside a 256-thread workgroup: wave 0 polls flags, lane kSignalLane (wave 1) stores
+// flags to peers, lane kGrabLane (wave 2) issues work grabs.  gfx9-family waves count loads,
+// stores and returning atomics in ONE in-order vmcnt, so a poll issued by the wave that just
+// stored a flag over xGMI (or issued a grab) would first wait for that store's acknowledgement:
+// separate waves keep the three latencies from adding up.
+constexpr int kSignalLane = 64, kGrabLane = 128;
+
+template <typename A>
+__device__ __forceinline__ void grab_issue(const A &a, int word, uint32_t &pending)
+{
+    if (threadIdx.x == kGrabLane)
+        pending = __hip_atomic_fetch_add(a.ep_ctr + word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t grab_take(uint32_t pending)
 {
     __shared__ uint32_t s_v;
     __syncthreads();  // every thread has read the previous value
-    if (threadIdx.x == 0)
-        s_v = __hip_atomic_fetch_add(a.ep_ctr + word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == kGrabLane) s_v = pending;
     __syncthreads();
-    return s_v;
+    // Block-uniform: keep it (and everything derived from it) in scalar registers.
+    return __builtin_amdgcn_readfirstlane(s_v);
+}
+
+template <typename A>
+__device__ __forceinline__ uint32_t block_grab(const A &a, int word)
+{
+    uint32_t pending = 0;
+    grab_issue(a, word, pending);
+    return grab_take(pending);
+}
+
+// Development trace (ReduceArgs::trace, set_param "trace_buffer"): per workgroup, s_memrealtime
+// (100 MHz) at kernel entry, start satisfied, RS done, AG done, finish entered, and — for the
+// launch's last workgroup — after the done handshake.  8 u64 slots per workgroup.
+__device__ __forceinline__ void trace_mark(uint64_t *tr, int k)
+{
+    if (tr && threadIdx.x == 0) tr[(size_t) blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Start of a collective launch (replaces the start half of ishmemi_team_sync,
@@ -279,13 +340,53 @@ __device__ __forceinline__ uint32_t block_grab(const A &a, int word)
 // other member — this member's source is final, since the launch runs after everything before it
 // on the stream — and every workgroup waits until every member has announced the same launch.
 // No workgroup waits for a particular peer workgroup, so residency never matters.
+// Workgroup 0 announces at once (no atomic on its path); whichever other workgroup runs first
+// announces too (its "started" add returns 0), so the announcement never waits for a particular
+// workgroup to be resident.  The duplicate stores the same epoch.
+// The announcement is stored into kEpReplicas start slots of every peer (the signalling wave,
+// one slot per lane), and workgroup b polls slot b mod kEpReplicas: hundreds of workgroups
+// polling one 64-B line would queue on it.
+// One whole wave: this member's start announcement into every peer's kEpReplicas start slots,
+// then the local mark "announced in epoch ep" (word 1 of every epoch replica line).
+template <typename A>
+__device__ __forceinline__ void announce_wave(const A &a, uint32_t ep)
+{
+    const int r = threadIdx.x & 63;
+    for (int j = 0; j < a.p; ++j) {
+        if (j == a.me) continue;
+        __hip_atomic_store(flag_slot(a.peer_flags[j], kPhaseStart, r) + a.me, ep, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __hip_atomic_store(a.ep_ctr + (kEpRepLine + r) * kLineWords + 1, ep, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Workgroup 0 announces at once, from the signalling wave (no atomic on any workgroup's path:
+// 255 workgroups adding to one "started" word cost ~2.5 us here).  Every other workgroup, once
+// it has seen every peer, checks the local "announced" mark and announces itself if it is not
+// there yet (its PE must not do work peers depend on while peers still wait for it: workgroup 0
+// may be queued behind other work).  A workgroup that has waited kAnnouncePatience without
+// seeing every peer announces too — if workgroup 0 is not resident
+// (CUs held by other work), any resident workgroup of the launch eventually speaks for it;
+// duplicates store the same epoch.
+constexpr uint64_t kAnnouncePatience = 2000;  // 20 us of s_memrealtime
+
 template <typename A>
 __device__ bool launch_start(const A &a, uint32_t ep)
 {
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(a.ep_ctr + kEpStarted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-        push_flag(a, kPhaseStart, 0, ep, false);
-    return block_wait(a, ep, kPhaseStart, 0, -1);
+    if (blockIdx.x == 0 && threadIdx.x >= kSignalLane && threadIdx.x < kSignalLane + 64)
+        announce_wave(a, ep);
+    const int slot = (int) (blockIdx.x % kEpReplicas);
+    int st = block_wait_ex(a, ep, kPhaseStart, slot, -1, blockIdx.x == 0 ? 0 : kAnnouncePatience);
+    if (st == 2) {
+        if (threadIdx.x >= kSignalLane && threadIdx.x < kSignalLane + 64) announce_wave(a, ep);
+        st = block_wait_ex(a, ep, kPhaseStart, slot, -1, 0);
+    } else if (st == 0 && blockIdx.x != 0 && threadIdx.x >= kSignalLane && threadIdx.x < kSignalLane + 64) {
+        const uint32_t mark = __hip_atomic_load(a.ep_ctr + (kEpRepLine + slot) * kLineWords + 1,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_readfirstlane(mark) != ep) announce_wave(a, ep);
+    }
+    return st == 0;
 }
 
 // End of a collective launch; every workgroup calls it once.  The last workgroup to finish
@@ -298,14 +399,28 @@ template <typename A>
 __device__ void launch_finish(const A &a, uint32_t ep)
 {
     __shared__ int s_last;
-    drain_block();
-    if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(a.ep_ctr + kEpDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 gridDim.x - 1;
+    // No store drain: "done" speaks for this workgroup's LOADS of peer memory, all of which have
+    // returned (their values were stored or folded); its own stores complete with the kernel.
     __syncthreads();
-    if (!s_last) return;
-    if (threadIdx.x == 0) push_flag(a, kPhaseEnd, 0, ep, false);
+    if (threadIdx.x == 0) {
+        // Finished count sharded by blockIdx mod kEpShards (~ per XCD under round-robin
+        // dispatch); the workgroup completing a shard counts it at the top line.
+        const uint32_t k = blockIdx.x % kEpShards;
+        const uint32_t in_shard = (gridDim.x - k + kEpShards - 1) / kEpShards;
+        int last = 0;
+        if (__hip_atomic_fetch_add(a.ep_ctr + (kEpShardLine + k) * kLineWords, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) == in_shard - 1) {
+            const uint32_t shards = gridDim.x < (uint32_t) kEpShards ? gridDim.x : (uint32_t) kEpShards;
+            last = __hip_atomic_fetch_add(a.ep_ctr + kEpTopLine * kLineWords, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) == shards - 1;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(s_last)) return;
+    if (threadIdx.x == kSignalLane) push_flag(a, kPhaseEnd, 0, ep, false);
     const bool ok = block_wait(a, ep, kPhaseEnd, 0, -1);
+    if constexpr (std::is_same_v<A, ReduceArgs>) trace_mark(a.trace, 5);
     if (threadIdx.x == 0) {
         uint32_t *w = a.ep_ctr;
         const bool failed =
@@ -313,8 +428,11 @@ __device__ void launch_finish(const A &a, uint32_t ep)
         if (failed && a.ret) __hip_atomic_fetch_or(a.ret, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         for (int k = kEpDone; k < kEpWords; ++k)
             __hip_atomic_store(w + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(w + kEpEpoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int k = 0; k <= kEpShards; ++k)  // the shards and the top line
+            __hip_atomic_store(w + (kEpShardLine + k) * kLineWords, 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (threadIdx.x < 64) publish_epoch_wave(a, ep);
 }
 
 // Standalone barrier of one workgroup (team_sync_kernel): member me stores the call's epoch into
@@ -323,7 +441,7 @@ template <typename A>
 __device__ bool pe_barrier(const A &a, uint32_t ep, int phase, int slot)
 {
     drain_block();
-    if (threadIdx.x == 0) push_flag(a, phase, slot, ep, false);
+    if (threadIdx.x == kSignalLane) push_flag(a, phase, slot, ep, false);
     return block_wait(a, ep, phase, slot, -1);
 }
 
@@ -336,8 +454,13 @@ __device__ __forceinline__ void rs_tile(const ReduceArgs &a, uint64_t t0, uint64
 {
     using Item = std::conditional_t<VEC, Vec<T>, T>;
     constexpr uint64_t IB = sizeof(Item);
-    constexpr int H = sizeof(T) >= 4 ? 2 : 1;  // items per thread per step: P * H staged in registers
-    const int tid = threadIdx.x;
+    // Items per thread per step: P * H = 8 loads staged in registers for P in {2, 4, 8}
+    // (MI355X_MICROARCH.md: keep >= 8 loads per lane outstanding on streamed hand-offs; more
+    // pushed the kernel past 128 VGPRs, i.e. below 4 workgroups per CU).
+    constexpr int H = sizeof(T) >= 4 ? (P <= 2 ? 4 : P == 4 ? 2 : 1) : 1;
+    const uint32_t tid = threadIdx.x;
+    // Items left in this tile (wave-uniform, <= kTile): 32-bit per-lane bounds checks.
+    const uint32_t lim = (uint32_t) min<uint64_t>(ce - t0, kTile);
 #pragma unroll
     for (int h = 0; h < kUnroll / H; ++h) {
         Item x[H][P];
@@ -349,15 +472,15 @@ __device__ __forceinline__ void rs_tile(const ReduceArgs &a, uint64_t t0, uint64
                 const Item *lp = (const Item *) base;
 #pragma unroll
                 for (int u = 0; u < H; ++u) {
-                    const uint64_t e = (uint64_t) (h * H + u) * kBlock + tid;
-                    if (t0 + e < ce) x[u][k] = lp[e];
+                    const uint32_t e = (uint32_t) (h * H + u) * kBlock + tid;
+                    if (e < lim) x[u][k] = lp[e];
                 }
             } else {
                 const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
 #pragma unroll
                 for (int u = 0; u < H; ++u) {
-                    const uint64_t e = (uint64_t) (h * H + u) * kBlock + tid;
-                    if (t0 + e < ce) x[u][k] = cload<Item>(r, (uint32_t) (e * IB));
+                    const uint32_t e = (uint32_t) (h * H + u) * kBlock + tid;
+                    if (e < lim) x[u][k] = cload<Item>(r, e * (uint32_t) IB);
                 }
             }
         }
@@ -367,8 +490,8 @@ __device__ __forceinline__ void rs_tile(const ReduceArgs &a, uint64_t t0, uint64
             Item acc = x[u][(P - R) % P];  // member 0
 #pragma unroll
             for (int j = 1; j < P; ++j) acc = op1<T, OP>(acc, x[u][(j - R + P) % P]);
-            const uint64_t e = (uint64_t) (h * H + u) * kBlock + tid;
-            if (t0 + e < ce) wt_store(dr, (uint32_t) (e * IB), acc);
+            const uint32_t e = (uint32_t) (h * H + u) * kBlock + tid;
+            if (e < lim) wt_store(dr, e * (uint32_t) IB, acc);
         }
     }
 }
@@ -396,7 +519,9 @@ __device__ __forceinline__ void rs_tile_any(const ReduceArgs &a, int rot, uint64
     constexpr uint64_t IB = sizeof(Item);
     constexpr bool kOrderFree =
         !(std::is_floating_point_v<T> && (OP == ISHMEMI_OP_SUM || OP == ISHMEMI_OP_PROD));
-    const int tid = threadIdx.x, p = a.p;
+    const uint32_t tid = threadIdx.x;
+    const int p = a.p;
+    const uint32_t lim = (uint32_t) min<uint64_t>(ce - t0, kTile);
     Item acc[kUnroll];
     for (int k = 0; k < p; ++k) {
         const int j = kOrderFree ? (rot + k) % p : k;
@@ -406,15 +531,15 @@ __device__ __forceinline__ void rs_tile_any(const ReduceArgs &a, int rot, uint64
             const Item *lp = (const Item *) base;
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
-                const uint64_t e = (uint64_t) u * kBlock + tid;
-                if (t0 + e < ce) x[u] = lp[e];
+                const uint32_t e = (uint32_t) u * kBlock + tid;
+                if (e < lim) x[u] = lp[e];
             }
         } else {
             const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
-                const uint64_t e = (uint64_t) u * kBlock + tid;
-                if (t0 + e < ce) x[u] = cload<Item>(r, (uint32_t) (e * IB));
+                const uint32_t e = (uint32_t) u * kBlock + tid;
+                if (e < lim) x[u] = cload<Item>(r, e * (uint32_t) IB);
             }
         }
         if (k == 0) {
@@ -428,8 +553,8 @@ __device__ __forceinline__ void rs_tile_any(const ReduceArgs &a, int rot, uint64
     const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + head_bytes + t0 * IB));
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-        const uint64_t e = (uint64_t) u * kBlock + tid;
-        if (t0 + e < ce) wt_store(dr, (uint32_t) (e * IB), acc[u]);
+        const uint32_t e = (uint32_t) u * kBlock + tid;
+        if (e < lim) wt_store(dr, e * (uint32_t) IB, acc[u]);
     }
 }
 
@@ -449,121 +574,262 @@ __device__ __forceinline__ uint32_t nsegs(uint64_t len, uint64_t seg)
 
 // ---------------------------------------------------------------------------------------------
 // Multi-PE reduce-scatter + all-gather (one launch per collective).
-//   start    - launch_start: every member has announced this launch (sources final).
-//   RS       - workgroups grab segments of chunk `me` from a work counter, fold each segment of
-//              every member's source in canonical team order (peers via sc0 sc1 loads), store
-//              it write-through into own dest, drain, and push "segment s ready" to every peer.
-//   AG       - workgroups grab (peer j, segment s) items, round-robin over the peers so every
-//              link is busy, wait for j's "segment s ready" in the LOCAL flag row and pull it
-//              from j's dest.  In place, the AG store into chunk j overwrites bytes member j
-//              read in its RS of segment s, which it had finished before publishing s.
-//   finish   - launch_finish: the last workgroup exchanges "done reading" with every member.
-// Every workgroup grabs RS work before AG work, so any workgroup waiting in AG implies that all
-// RS segments are held by running workgroups that wait for nothing but the start flags: the
-// launch completes whatever subset of its grid (and of its peers' grids) is resident.
+//   start  - launch_start: every member has announced this launch (sources final).
+//   RS     - segment b of chunk `me` (contiguous tiles) belongs to workgroup b: it claims it (one
+//            uncontended atomic exchange of the launch's epoch into the segment's claim word),
+//            folds it from every member's source in canonical team order (peers via sc0 sc1
+//            loads), stores it write-through into own dest, drains and pushes "segment b ready"
+//            to every peer.  Segments G.. are grabbed from a work counter by whichever workgroup
+//            is free (one grab per segment, in flight while the previous segment streams).
+//   AG     - item i = (peer j, segment s), round-robin over the peers so every link is busy;
+//            item b is workgroup b's, items G.. are grabbed.  It waits for j's "segment s ready"
+//            in the LOCAL flag row and pulls the segment from j's dest.  In place, the AG store
+//            into chunk j overwrites bytes member j read in its RS of segment s, which it finished
+//            before publishing s.
+//   finish - launch_finish: the last workgroup exchanges "done reading" with every member.
+// Owned first segments cost no contended atomics when every workgroup has one segment (round
+// 2's first version grabbed every segment from one counter: 256 workgroups x 2 grabs queued on
+// one line, +6 us at 4 MiB); grabbing the rest keeps large arrays balanced when workgroups (or
+// co-located PEs) run at uneven speeds (all-static ownership ran 1 GiB at 8 PEs on one GPU in
+// 7.2 ms against 3.9 ms grabbed).  Residency: a peer only ever waits for RS segments; grabbed
+// ones are held by running workgroups, and an AG waiter that has waited kStealPatience claims and
+// reduces any still-unclaimed owned segment of its own PE (owner not resident) — the claim word
+// makes every owned segment reduced exactly once.
 // ---------------------------------------------------------------------------------------------
+// Long enough that launch skew between PEs and ordinary waits never trigger it (a steal scans
+// claim words); short against the device timeout.
+constexpr uint64_t kStealPatience = 10000;  // 100 us of s_memrealtime
+
+template <typename A>
+__device__ __forceinline__ uint32_t *claim_word(const A &a, uint32_t s)
+{
+    return a.ep_ctr + kEpClaimLine * kLineWords + s;
+}
+
+// Lane kGrabLane issues the claim of segment s (old value returned later); claim_take
+// broadcasts whether this workgroup won it.
+template <typename A>
+__device__ __forceinline__ void claim_issue(const A &a, uint32_t ep, uint32_t s, uint32_t &pending)
+{
+    if (threadIdx.x == kGrabLane)
+        pending = __hip_atomic_exchange(claim_word(a, s), ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool claim_take(uint32_t pending, uint32_t ep)
+{
+    return grab_take(pending) != ep;
+}
+
+// Steal: wave 2 scans the claim words of [0, nseg) from the END (owners claim in increasing
+// order, so unclaimed segments gather there) for one not yet claimed by this launch and claims
+// it.  Returns the segment, or nseg if every segment is claimed.  All threads call.
+template <typename A>
+__device__ uint32_t steal_segment(const A &a, uint32_t ep, uint32_t nseg)
+{
+    __shared__ uint32_t s_found;
+    if (threadIdx.x == kGrabLane) s_found = nseg;
+    __syncthreads();
+    if (threadIdx.x >= kGrabLane && threadIdx.x < kGrabLane + 64) {
+        const uint32_t lane = threadIdx.x - kGrabLane;
+        for (uint32_t top = nseg; top > 0; top = top > 64 ? top - 64 : 0) {
+            const uint32_t s = top - 1 - lane;
+            bool open = false;
+            if (lane < top)
+                open = __hip_atomic_load(claim_word(a, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep;
+            uint64_t mask = __ballot(open);
+            bool got = false;
+            while (mask && !got) {
+                const uint32_t l = (uint32_t) __builtin_ctzll(mask);
+                uint32_t old = ep;
+                if (lane == l) old = __hip_atomic_exchange(claim_word(a, s), ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                got = __builtin_amdgcn_readlane(old, l) != ep;
+                if (got && lane == l) s_found = s;
+                mask &= mask - 1;
+            }
+            if (got) break;
+        }
+    }
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(s_found);
+}
+
+// One reduce-scatter segment: tiles s, s + nseg, ... of [cs, ce), the unaligned head / tail with
+// segment 0, then (not one-shot) drain and publish "segment s ready".
 template <typename T, int OP, bool VEC, int P>
-__global__ __launch_bounds__(kBlock) __attribute__((flatten)) void allreduce_kernel(ReduceArgs a)
+__device__ __forceinline__ void rs_segment(const ReduceArgs &a, uint32_t ep, uint32_t s, uint32_t nseg,
+                                           uint64_t cs, uint64_t ce, uint64_t head_bytes, bool one)
+{
+    const int tid = threadIdx.x, p = a.p, me = a.me;
+    // Load order rotated by segment: concurrently folded segments read from all members (all
+    // links) at once; the fold order stays canonical 0..p-1.  A segment is contiguous (each
+    // workgroup stays inside one 2 MiB page of every member's array for many tiles: a strided
+    // tile set, tried, ran 7 % (2 PEs) to 30 % (8 PEs) slower at 1 GiB).
+    const int rot = (int) (s % (uint32_t) p);
+    const uint64_t ss = cs + (uint64_t) s * a.seg_items, se = min(ss + a.seg_items, ce);
+    for (uint64_t t0 = ss; t0 < se; t0 += kTile) {
+        const uint64_t te = min(t0 + kTile, se);
+        if constexpr (P > 0) rs_tile_dispatch<T, OP, VEC, P>(a, rot, t0, te, head_bytes);
+        else rs_tile_any<T, OP, VEC>(a, rot, t0, te, head_bytes);
+    }
+    (void) nseg;
+    // Unaligned head (owned by member 0) and tail (owned by member p-1; one-shot: both by every
+    // member), element-wise, with segment 0.  Descriptors are based at the region (offsets
+    // < 16 B), never at the array start (a > 2 GiB array exceeds a descriptor's range).
+    if (VEC && s == 0) {
+        const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
+        for (int region = 0; region < 2; ++region) {
+            const bool owner = one || (region == 0 ? me == 0 : me == p - 1);
+            const uint64_t cnt = region == 0 ? a.head : a.tail;
+            if (!owner || (uint64_t) tid >= cnt) continue;
+            const uint64_t rbase = (region == 0 ? 0 : tail_off) * sizeof(T);
+            const uint32_t off = (uint32_t) (tid * sizeof(T));
+            T acc = T();
+            for (int j = 0; j < p; ++j) {
+                T x;
+                if (j == me) x = ((const T *) (a.src[j] + rbase))[tid];
+                else x = cload<T>(make_rsrc(uniform_ptr(a.src[j] + rbase)), off);
+                acc = (j == 0) ? x : op1<T, OP>(acc, x);
+            }
+            wt_store(make_rsrc(uniform_ptr(a.dst + rbase)), off, acc);
+        }
+    }
+    if (!one) {
+        drain_block();
+        if (tid == kSignalLane) {
+            release_system();
+            push_flag(a, kPhaseMid, (int) s, ep, false);
+        }
+    }
+}
+
+template <typename T, int OP, bool VEC, int P>
+__global__ __launch_bounds__(kBlock, sizeof(T) == 1 ? 2 : 3) __attribute__((flatten)) void allreduce_kernel(ReduceArgs a)
 {
     using Item = std::conditional_t<VEC, Vec<T>, T>;
     constexpr uint64_t IB = sizeof(Item);
     const int tid = threadIdx.x;
     const int p = a.p, me = a.me;
+    const uint32_t G = gridDim.x, b = blockIdx.x;
     const uint64_t head_bytes = VEC ? a.head * sizeof(T) : 0;
     const uint64_t seg = a.seg_items;
     const bool one = a.oneshot != 0;
+    trace_mark(a.trace, 0);
     const uint32_t ep = kernel_epoch(a);
-    bool ok = launch_start(a, ep);
+    trace_mark(a.trace, 6);
 
     // ---- reduce-scatter of chunk `me` (one-shot: the whole array) ----
     uint64_t cs = 0, ce = a.nitems;
     if (!one) chunk_of(a, me, cs, ce);
     const uint32_t nseg = nsegs(ce - cs, seg);
-    while (ok) {
-        const uint32_t s = block_grab(a, kEpRsHead);
-        if (s >= nseg) break;
-        const uint64_t ss = cs + (uint64_t) s * seg, se = min(ss + seg, ce);
-        // Load order rotated by segment: concurrently folded segments read from all members
-        // (all links) at once; the fold order stays canonical 0..p-1.
-        const int rot = (int) (s % (uint32_t) p);
-        for (uint64_t t0 = ss; t0 < se; t0 += kTile) {
-            if constexpr (P > 0) rs_tile_dispatch<T, OP, VEC, P>(a, rot, t0, se, head_bytes);
-            else rs_tile_any<T, OP, VEC>(a, rot, t0, se, head_bytes);
-        }
-        // Unaligned head (owned by member 0) and tail (owned by member p-1; one-shot: both by
-        // every member), element-wise, with segment 0.  Descriptors are based at the region
-        // (offsets < 16 B), never at the array start (a > 2 GiB array exceeds a descriptor).
-        if (VEC && s == 0) {
-            const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
-            for (int region = 0; region < 2; ++region) {
-                const bool owner = one || (region == 0 ? me == 0 : me == p - 1);
-                const uint64_t cnt = region == 0 ? a.head : a.tail;
-                if (!owner || (uint64_t) tid >= cnt) continue;
-                const uint64_t rbase = (region == 0 ? 0 : tail_off) * sizeof(T);
-                const uint32_t off = (uint32_t) (tid * sizeof(T));
-                T acc = T();
-                for (int j = 0; j < p; ++j) {
-                    T x;
-                    if (j == me) x = ((const T *) (a.src[j] + rbase))[tid];
-                    else x = cload<T>(make_rsrc(uniform_ptr(a.src[j] + rbase)), off);
-                    acc = (j == 0) ? x : op1<T, OP>(acc, x);
-                }
-                wt_store(make_rsrc(uniform_ptr(a.dst + rbase)), off, acc);
-            }
-        }
-        if (!one) {
-            drain_block();
-            if (tid == 0) {
-                release_system();
-                push_flag(a, kPhaseMid, (int) s, ep, false);
-            }
-        }
-    }
+    uint32_t pending = 0, pclaim = 0;
+    if (b < nseg) claim_issue(a, ep, b, pclaim);  // overlaps the start wait
+    bool ok = launch_start(a, ep);
+    trace_mark(a.trace, 1);
 
-    // ---- all-gather: pull every other member's reduced segments from its dest ----
-    if (ok && !one) {
-        const uint32_t per_peer = nsegs(min(a.items_per_chunk, a.nitems), seg);  // chunk 0 is the largest
-        const uint32_t total = (uint32_t) (p - 1) * per_peer;
-        for (;;) {
-            const uint32_t i = block_grab(a, kEpAgHead);
-            if (i >= total) break;
-            const int j = (me + 1 + (int) (i % (uint32_t) (p - 1))) % p;
-            const uint32_t s = i / (uint32_t) (p - 1);
+    // One work loop (so the segment body and the all-gather body are each instantiated once):
+    //   RS_OWN - segment b, this workgroup's own (claimed, so a stealer can take it if this
+    //            workgroup never becomes resident);
+    //   RS_DYN - segments G.. grabbed from the head by whoever is free (they balance uneven
+    //            workgroup speeds on large arrays; no claim: the head hands each out once);
+    //   AG     - item b, then items G.. grabbed; a wait longer than kStealPatience first reduces
+    //            an unclaimed owned segment of this PE (its owner is not resident), then resumes.
+    enum { kRsOwn, kRsDyn, kAg } state = kRsOwn;
+    const bool dyn_rs = nseg > G;
+    if (dyn_rs) grab_issue(a, kEpRsHead, pending);
+    const uint32_t per_peer = nsegs(min(a.items_per_chunk, a.nitems), seg);  // chunk 0 is the largest
+    const uint32_t total = one ? 0 : (uint32_t) (p - 1) * per_peer;
+    const bool dyn_ag = total > G;
+    uint32_t item = b;          // current all-gather item (valid when have_item)
+    bool have_item = false, ag_first = true, may_steal = true;
+    while (ok) {
+        uint32_t rs = 0xFFFFFFFFu;  // segment to reduce in this pass, if any
+        if (state == kRsOwn) {
+            state = kRsDyn;
+            if (b < nseg && claim_take(pclaim, ep)) rs = b;
+        } else if (state == kRsDyn) {
+            if (dyn_rs) {
+                const uint32_t s = G + grab_take(pending);
+                if (s < nseg) {
+                    grab_issue(a, kEpRsHead, pending);  // next grab in flight while this streams
+                    rs = s;
+                }
+            }
+            if (rs == 0xFFFFFFFFu) {
+                state = kAg;
+                if (dyn_ag) grab_issue(a, kEpAgHead, pending);
+            }
+        } else {
+            if (!have_item) {
+                if (ag_first) {
+                    ag_first = false;
+                    item = b;
+                } else {
+                    if (!dyn_ag) break;
+                    item = G + grab_take(pending);
+                    if (item < total) grab_issue(a, kEpAgHead, pending);
+                }
+                if (item >= total) break;
+                have_item = true;
+            }
+            const int j = (me + 1 + (int) (item % (uint32_t) (p - 1))) % p;
+            const uint32_t s = item / (uint32_t) (p - 1);
             uint64_t js, je;
             chunk_of(a, j, js, je);
-            if (s >= nsegs(je - js, seg)) continue;
-            if (!block_wait(a, ep, kPhaseMid, (int) s, j)) {
+            if (s >= nsegs(je - js, seg)) {
+                have_item = false;
+                continue;
+            }
+            const int st = block_wait_ex(a, ep, kPhaseMid, (int) s, j, may_steal ? kStealPatience : 0);
+            if (st == 1) {
                 ok = false;
                 break;
             }
-            const uint64_t ss = js + (uint64_t) s * seg, se = min(ss + seg, je);
-            for (uint64_t t0 = ss; t0 < se; t0 += kTile) {
-                const __amdgpu_buffer_rsrc_t r = make_rsrc(uniform_ptr(a.dstp[j] + head_bytes + t0 * IB));
-                Item x[kUnroll];
+            if (st == 2) {
+                // Waited long: reduce one of this PE's owned segments nobody has claimed, so
+                // peers stuck on it progress; then wait for the same item again.
+                const uint32_t nown = nseg < G ? nseg : G;
+                const uint32_t t = steal_segment(a, ep, nown);
+                if (t < nown) rs = t;
+                else may_steal = false;
+            } else {
+                have_item = false;
+                // The segment's tiles, two per step: 8 loads per lane in flight.
+                const uint64_t ss = js + (uint64_t) s * seg, se = min(ss + seg, je);
+                for (uint64_t t = ss; t < se; t += 2 * kTile) {
+                    // Two tiles in one descriptor window (offsets < 32 KiB): 8 loads per lane.
+                    constexpr int U = 2 * kUnroll;
+                    const uint32_t lim = (uint32_t) min<uint64_t>(se - t, 2 * kTile);
+                    const __amdgpu_buffer_rsrc_t r = make_rsrc(uniform_ptr(a.dstp[j] + head_bytes + t * IB));
+                    Item x[U];
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const uint64_t k = (uint64_t) u * kBlock + tid;
-                    if (t0 + k < se) x[u] = cload<Item>(r, (uint32_t) (k * IB));
-                }
-                const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + head_bytes + t0 * IB));
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t k = (uint32_t) u * kBlock + (uint32_t) tid;
+                        if (k < lim) x[u] = cload<Item>(r, k * (uint32_t) IB);
+                    }
+                    const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + head_bytes + t * IB));
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const uint64_t k = (uint64_t) u * kBlock + tid;
-                    if (t0 + k < se) wt_store(dr, (uint32_t) (k * IB), x[u]);
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t k = (uint32_t) u * kBlock + (uint32_t) tid;
+                        if (k < lim) wt_store(dr, k * (uint32_t) IB, x[u]);
+                    }
                 }
-            }
-            if (VEC && s == 0) {
-                const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
-                const uint64_t rbase = (j == 0 ? 0 : tail_off) * sizeof(T);
-                const bool do_head = (j == 0) && ((uint64_t) tid < a.head);
-                const bool do_tail = (j == p - 1) && ((uint64_t) tid < a.tail);
-                if (do_head || do_tail)
-                    ((T *) (a.dst + rbase))[tid] =
-                        cload<T>(make_rsrc(uniform_ptr(a.dstp[j] + rbase)), (uint32_t) (tid * sizeof(T)));
+                if (VEC && s == 0) {
+                    const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
+                    const uint64_t rbase = (j == 0 ? 0 : tail_off) * sizeof(T);
+                    const bool do_head = (j == 0) && ((uint64_t) tid < a.head);
+                    const bool do_tail = (j == p - 1) && ((uint64_t) tid < a.tail);
+                    if (do_head || do_tail)
+                        ((T *) (a.dst + rbase))[tid] =
+                            cload<T>(make_rsrc(uniform_ptr(a.dstp[j] + rbase)), (uint32_t) (tid * sizeof(T)));
+                }
             }
         }
+        if (rs != 0xFFFFFFFFu) rs_segment<T, OP, VEC, P>(a, ep, rs, nseg, cs, ce, head_bytes, one);
     }
+    trace_mark(a.trace, 2);
+    trace_mark(a.trace, 3);
     launch_finish(a, ep);
+    trace_mark(a.trace, 4);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -728,29 +994,44 @@ __global__ __launch_bounds__(kBlock) void team_sync_kernel(ReduceArgs a)
 template <int OP, typename S, typename U>
 using Canon = std::conditional_t<(OP == ISHMEMI_OP_MAX || OP == ISHMEMI_OP_MIN), S, U>;
 
-// Workgroups of `kernel` that are resident at once on this device (cached per kernel address),
-// divided among the PEs sharing the device.  The collectives are correct with any residency of
-// their own grid (they grab work; nothing is paired); the clamp avoids launching workgroups that
-// would find no work left, and keeps co-located PEs' launches from crowding each other out.  One block per CU of margin:
-// the occupancy API over-reports by one block per CU for SGPR-heavy 256-thread kernels on
-// ROCm 7.2 (MI355X_MICROARCH.md, residency).
+// Workgroups of `kernel` that are resident at once on this device (occupancy API, cached per
+// kernel address), divided among the PEs sharing the device.  The collectives are correct with
+// any residency of their grid (owned work can be stolen, the rest is grabbed; nothing is paired),
+// so the answer need not be exact (the API can over-report by one block per CU for SGPR-heavy
+// kernels, MI355X_MICROARCH.md residency): the clamp only avoids launching workgroups that would
+// queue behind the first wave, and keeps co-located PEs' launches from crowding each other out.
 inline int resident_blocks_of(const void *kernel)
 {
     static std::mutex mu;
     static std::map<const void *, int> cache;
+    static int cus = 0;
     std::lock_guard<std::mutex> lk(mu);
+    if (cus <= 0) {
+        int dev = 0;
+        (void) hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+            (void) hipGetLastError();
+            cus = 1;
+        }
+    }
     auto it = cache.find(kernel);
-    if (it != cache.end()) return std::max(1, it->second / device_share());
-    int dev = 0, cus = 0, per = 0;
-    (void) hipGetDevice(&dev);
-    (void) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (it != cache.end()) {
+        const int per = it->second, pe_share = device_share();
+        const int per_cu = pe_share > 1 && per > 1 ? per - 1 : per;
+        return std::max(1, per_cu * std::max(cus, 1) / pe_share);
+    }
+    int per = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess) {
         (void) hipGetLastError();
         per = 1;
     }
-    const int n = std::max(1, (per > 1 ? per - 1 : 1) * std::max(cus, 1));
-    cache[kernel] = n;
-    return std::max(1, n / device_share());
+    cache[kernel] = std::max(per, 1);
+    // PEs sharing the GPU: one block per CU of margin, so every co-located PE's grid is
+    // resident at once even where the API over-reports — a PE none of whose workgroups is
+    // resident could not even announce its launch while its peers' workgroups wait for it.
+    const int pe_share = device_share();
+    const int per_cu = pe_share > 1 && per > 1 ? per - 1 : std::max(per, 1);
+    return std::max(1, per_cu * std::max(cus, 1) / pe_share);
 }
 
 template <typename K>
@@ -762,7 +1043,17 @@ int resident_blocks(K kernel)
 template <typename K>
 hipError_t launch_resident(K kernel, const ReduceArgs &a, int grid, hipStream_t s)
 {
-    grid = std::min(grid, resident_blocks(kernel));
+    // Balanced waves of grabs: the work list (the reduce-scatter segments of one chunk, or the
+    // all-gather items when those fit the grid at once) is split into equal waves, so no wave
+    // leaves most workgroups idle (1024 segments on a 768-workgroup cap would run one full wave
+    // and one a third full: 512 workgroups x 2 instead).
+    const uint64_t cap = (uint64_t) std::max(1, std::min(grid, resident_blocks(kernel)));
+    const uint64_t len = a.oneshot ? a.nitems : std::min(a.items_per_chunk, a.nitems);
+    const uint64_t nseg = std::max<uint64_t>(1, (len + a.seg_items - 1) / a.seg_items);
+    const uint64_t ag = a.oneshot ? 0 : nseg * (uint64_t) (a.p - 1);
+    const uint64_t work = ag > nseg && ag <= cap ? ag : nseg;
+    const uint64_t waves = (work + cap - 1) / cap;
+    grid = (int) std::max<uint64_t>(1, (work + waves - 1) / waves);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }

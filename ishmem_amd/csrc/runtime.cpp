@@ -16,6 +16,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "bootstrap.h"
 #include "kernels.h"
@@ -116,7 +117,7 @@ struct State {
     uint32_t *err_dev = nullptr;
     ishmemi_c_device_ctx_t *dctx = nullptr;  // device copy of the device-API context
     uint32_t *dev_epochs = nullptr;
-    uint32_t *kern_ep = nullptr;  // [team][kEpWords] launch words of the host-launched kernels
+    uint32_t *kern_ep = nullptr;  // [team][kEpTeamWords] launch words of the host-launched kernels
 
     char *team_scratch = nullptr;  // small symmetric buffer for team-management collectives
     char *staging = nullptr;  // symmetric staging region for non-heap / host buffers
@@ -144,6 +145,7 @@ struct State {
     long long timeout_ms = 60000;
     int debug = 0;
     int error_count = 0;
+    uint64_t *trace = nullptr;  // development phase-timestamp buffer (device memory)
 };
 
 State &S()
@@ -309,7 +311,7 @@ int team_args(State &s, int team, ReduceArgs &a, std::string &why)
             return 1;
         }
     }
-    a.ep_ctr = s.kern_ep + (size_t) kEpWords * team;
+    a.ep_ctr = s.kern_ep + (size_t) kEpTeamWords * team;
     return 0;
 }
 
@@ -440,7 +442,7 @@ int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, si
     a.ret = ret;
     a.nbytes = bytes;
     a.timeout_ticks = (uint64_t) s.timeout_ms * 100000ull;
-    a.ep_ctr = s.kern_ep + (size_t) kEpWords * team;
+    a.ep_ctr = s.kern_ep + (size_t) kEpTeamWords * team;
     a.p = t.size;
     a.me = t.my_idx;
     HIP_TRY(launch_ll(op, dt, a, st));
@@ -466,6 +468,7 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     }
     a.dst = (char *) dst;
     a.ret = ret;
+    a.trace = s.trace;
     const void *srcs[1] = {src};
     Plan pl = make_plan(dst, srcs, 1, n, es, t.size, s.max_blocks, 0);
     a.head = pl.head;
@@ -782,6 +785,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
                                          std::max<long long>(0, env_ll("ISHMEM_LL_MAX_BYTES", (long long) kLLDefaultBytes)));
     s.debug = (int) env_ll("ISHMEM_DEBUG", 0);
+    s.trace = nullptr;
     s.stream_order = env_ll("ISHMEM_STREAM_ORDER", 0) != 0;
     s.oneshot_p2 = std::max<long long>(0, env_ll("ISHMEM_ONESHOT_P2_MAX_BYTES", 64ll << 20));
     s.staging_bytes = (parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20) + kHeapAlign - 1) &
@@ -952,8 +956,12 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.team_scratch = (char *) heap_alloc(s, kHeapAlign, kHeapAlign);
     if (!s.team_scratch) return 1;
     HIP_TRY(hipMalloc((void **) &s.dctx, sizeof(ishmemi_c_device_ctx_t)));
-    const size_t ep_bytes = (size_t) kEpWords * kMaxTeams * sizeof(uint32_t);
-    if (hipExtMallocWithFlags((void **) &s.kern_ep, ep_bytes, hipDeviceMallocUncached) != hipSuccess) {
+    // Launch words: local to this device, touched only by device-scope atomics (work grabs,
+    // counters) and system-scope loads/stores (the epoch), which do not depend on the memory
+    // type; ordinary device memory (ISHMEM_EP_UNCACHED=1: fine-grained uncached, for comparison).
+    const size_t ep_bytes = (size_t) kEpTeamWords * kMaxTeams * sizeof(uint32_t);
+    if (env_ll("ISHMEM_EP_UNCACHED", 0) == 0 ||
+        hipExtMallocWithFlags((void **) &s.kern_ep, ep_bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void) hipGetLastError();
         HIP_TRY(hipMalloc((void **) &s.kern_ep, ep_bytes));
     }
@@ -1214,7 +1222,7 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
             hipMemset(dev_flags(s.flags) + (size_t) slot * kDevFlagWordsPerTeam, 0,
                       kDevFlagWordsPerTeam * 4) != hipSuccess ||
             hipMemset(s.dev_epochs + slot, 0, sizeof(uint32_t)) != hipSuccess ||
-            hipMemset(s.kern_ep + (size_t) kEpWords * slot, 0, kEpWords * sizeof(uint32_t)) != hipSuccess ||
+            hipMemset(s.kern_ep + (size_t) kEpTeamWords * slot, 0, kEpTeamWords * sizeof(uint32_t)) != hipSuccess ||
             hipMemset(ll_ring(s.flags, slot), 0, kLLTeamBytes) != hipSuccess)
             return fail("team_split_strided: flag reset failed");
         if (sync_device_ctx(s)) return 1;
@@ -1301,10 +1309,10 @@ int ishmemi_c_resync(void)
     struct Epochs {
         uint32_t host[kMaxTeams], dev[kMaxTeams];
     } mine{}, all[kMaxPes];
-    uint32_t words[kMaxTeams * kEpWords];
-    HIP_TRY(hipMemcpy(words, s.kern_ep, sizeof(words), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> words((size_t) kMaxTeams * kEpTeamWords);
+    HIP_TRY(hipMemcpy(words.data(), s.kern_ep, words.size() * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(mine.dev, s.dev_epochs, sizeof(mine.dev), hipMemcpyDeviceToHost));
-    for (int t = 0; t < kMaxTeams; ++t) mine.host[t] = words[t * kEpWords + kEpEpoch];
+    for (int t = 0; t < kMaxTeams; ++t) mine.host[t] = words[(size_t) t * kEpTeamWords + kEpEpoch];
     if (s.npes > 1) {
         std::string err;
         if (s.boot.allgather(&mine, all, sizeof(Epochs), err)) return fail("resync: " + err);
@@ -1318,11 +1326,13 @@ int ishmemi_c_resync(void)
             h = newest(h, all[j].host[t]);
             d = newest(d, all[j].dev[t]);
         }
-        for (int k = 0; k < kEpWords; ++k) words[t * kEpWords + k] = 0;
-        words[t * kEpWords + kEpEpoch] = h;
+        uint32_t *w = words.data() + (size_t) t * kEpTeamWords;
+        for (int k = 0; k < kEpTeamWords; ++k) w[k] = 0;
+        w[kEpEpoch] = h;
+        for (int r = 0; r < kEpReplicas; ++r) w[(kEpRepLine + r) * kLineWords] = h;
         mine.dev[t] = d;
     }
-    HIP_TRY(hipMemcpy(s.kern_ep, words, sizeof(words), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s.kern_ep, words.data(), words.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(s.dev_epochs, mine.dev, sizeof(mine.dev), hipMemcpyHostToDevice));
     for (int t = 0; t <= kMaxTeams; ++t) __atomic_store_n(&s.err_host[t], 0u, __ATOMIC_RELEASE);
     HIP_TRY(hipDeviceSynchronize());
@@ -1456,6 +1466,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "oneshot_p2_max_bytes") s.oneshot_p2 = std::max<long long>(0, value);
     else if (n == "ll_max_bytes") s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes, std::max<long long>(0, value));
     else if (n == "debug") s.debug = (int) value;
+    else if (n == "trace_buffer") s.trace = (uint64_t *) (uintptr_t) value;
     else return fail("set_param: unknown parameter " + n);
     return 0;
 }
@@ -1473,6 +1484,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "flags_fine_grained") return s.flags_fine_grained ? 1 : 0;
     if (n == "staging_bytes") return (long long) s.staging_bytes;
     if (n == "heap_bytes") return (long long) s.heap_size;
+    if (n == "launch_words") return (long long) (uintptr_t) s.kern_ep;  // debug: device address
     if (n == "cu_count") {
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||

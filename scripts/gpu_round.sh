@@ -38,8 +38,9 @@ for s in $STEPS; do
             ISHMEM_BENCH_SAME_DEVICE=1 run bench_$s 900 python bench.py --gpus $np_ --steps 10 --warmup 3 \
                 --mib ${MIB:-1024} --sweep-max-mib ${SWEEP_MIB:-4096} ;;
     sweep1) run sweep1 300 python tools/sweep.py --max-mib 1024 ;;
-    sweep2) ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-256} run sweep2 600 python -m torch.distributed.run \
-                --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 tools/sweep.py --max-mib 256 ;;
+    sweep2|sweep4|sweep8) np_=${s#sweep}
+            ISHMEM_BENCH_SAME_DEVICE=1 run $s 600 python -m torch.distributed.run \
+                --nnodes=1 --nproc-per-node $np_ --master-addr 127.0.0.1 --master-port 2951$np_ tools/sweep.py --max-mib 256 ;;
     llcmp)  for np_ in 2 4; do for ll in 0 65536; do
               ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_MAX_BLOCKS=${MB:-128} ISHMEM_LL_MAX_BYTES=$ll run llcmp_p${np_}_ll${ll} 300 \
                 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np_ --master-addr 127.0.0.1 \
