@@ -929,8 +929,13 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
         const uint64_t off = item * 8;
         const uint64_t valid = a.nbytes - off < 8 ? a.nbytes - off : 8;
         uint64_t mine = 0;
-        if (valid == 8) mine = *(const uint64_t *) (a.src + off);
-        else memcpy(&mine, a.src + off, valid);
+        if (valid == 8) {
+            mine = *(const uint64_t *) (a.src + off);
+        } else {
+            // Ragged last item: byte assembly (a variable-length memcpy would go through scratch).
+            for (uint32_t k = 0; k < (uint32_t) valid; ++k)
+                mine |= (uint64_t) (uint8_t) a.src[off + k] << (8 * k);
+        }
         const uint64_t g0 = tag | (uint32_t) mine, g1 = tag | (uint32_t) (mine >> 32);
         for (int j = 0; j < p; ++j) {
             if (j == me) continue;
@@ -961,8 +966,11 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
             acc = (j == 0) ? x : fold8<T, OP>(acc, x);
         }
         if (ok) {
-            if (valid == 8) *(uint64_t *) (a.dst + off) = acc;
-            else memcpy(a.dst + off, &acc, valid);
+            if (valid == 8) {
+                *(uint64_t *) (a.dst + off) = acc;
+            } else {
+                for (uint32_t k = 0; k < (uint32_t) valid; ++k) a.dst[off + k] = (char) (acc >> (8 * k));
+            }
         }
     }
     // *ret was zeroed by the caller: any thread that failed marks it (sticky over launches).
