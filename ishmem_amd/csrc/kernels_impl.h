@@ -694,11 +694,14 @@ __device__ __forceinline__ void rs_segment(const ReduceArgs &a, uint32_t ep, uin
         }
     }
     if (!one) {
+        // Every payload store of the segment is a system-scope write-through store: once drained
+        // (vmcnt(0) in every wave) its bytes are past this XCD's L2, so the flag needs no release
+        // fence (MI355X_MICROARCH.md: handoff-flag, drained sc1 stores; cdna_hip_programming.md
+        // R1).  A system-scope release here is a buffer_wbl2 per segment — 1024 of them per
+        // launch, serialised per XCD — and made the reduce-scatter half the speed of the
+        // all-gather (same-device trace, 128 MiB: 2.2 against 5.3 TB/s).
         drain_block();
-        if (tid == kSignalLane) {
-            release_system();
-            push_flag(a, kPhaseMid, (int) s, ep, false);
-        }
+        if (tid == kSignalLane) push_flag(a, kPhaseMid, (int) s, ep, false);
     }
 }
 
@@ -741,6 +744,7 @@ __global__ __launch_bounds__(kBlock, sizeof(T) == 1 ? 2 : 3) __attribute__((flat
     const bool dyn_ag = total > G;
     uint32_t item = b;          // current all-gather item (valid when have_item)
     bool have_item = false, ag_first = true, may_steal = true;
+    uint64_t ag_wait = 0;  // trace only: ticks spent waiting for peers' segments
     while (ok) {
         uint32_t rs = 0xFFFFFFFFu;  // segment to reduce in this pass, if any
         if (state == kRsOwn) {
@@ -756,6 +760,7 @@ __global__ __launch_bounds__(kBlock, sizeof(T) == 1 ? 2 : 3) __attribute__((flat
             }
             if (rs == 0xFFFFFFFFu) {
                 state = kAg;
+                trace_mark(a.trace, 2);
                 if (dyn_ag) grab_issue(a, kEpAgHead, pending);
             }
         } else {
@@ -779,7 +784,9 @@ __global__ __launch_bounds__(kBlock, sizeof(T) == 1 ? 2 : 3) __attribute__((flat
                 have_item = false;
                 continue;
             }
+            const uint64_t w0 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
             const int st = block_wait_ex(a, ep, kPhaseMid, (int) s, j, may_steal ? kStealPatience : 0);
+            if (a.trace) ag_wait += __builtin_amdgcn_s_memrealtime() - w0;
             if (st == 1) {
                 ok = false;
                 break;
@@ -826,8 +833,8 @@ __global__ __launch_bounds__(kBlock, sizeof(T) == 1 ? 2 : 3) __attribute__((flat
         }
         if (rs != 0xFFFFFFFFu) rs_segment<T, OP, VEC, P>(a, ep, rs, nseg, cs, ce, head_bytes, one);
     }
-    trace_mark(a.trace, 2);
     trace_mark(a.trace, 3);
+    if (a.trace && tid == 0) a.trace[(size_t) b * 8 + 7] = ag_wait;
     launch_finish(a, ep);
     trace_mark(a.trace, 4);
 }
