@@ -68,7 +68,8 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
         def heap(n, dt):
             return ish.ishmem_malloc(max(1, n * np.dtype(oracle.NP[dt]).itemsize))
 
-        def check(tag, op, dt, srcs, got, golden=None):
+        def check(tag, op, dt, srcs, got, golden=None, me=None):
+            me = pe if me is None else me  # this PE's index in the team the srcs belong to
             ref = oracle.reduce_fold(op, dt, srcs, 0)  # canonical team order = every PE's result
             if not _bits_equal(got, ref):
                 bad = np.nonzero(got.view(np.uint8) != ref.view(np.uint8))[0]
@@ -78,10 +79,10 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 # The reference's own result on THIS PE folds self first, then team order
                 # (reduce_impl.h:247-253).  Both folds lie within fp_tolerance of the exact
                 # value, so they differ by at most twice that bound.
-                own = oracle.reduce_fold(op, dt, srcs, pe)
+                own = oracle.reduce_fold(op, dt, srcs, me)
                 tol = 2.0 * oracle.fp_tolerance(dt, op, srcs, ref)
                 if not np.all(np.abs(own.astype(np.float64) - got.astype(np.float64)) <= tol):
-                    fails.append(f"pe{pe} {tag}: outside tolerance of the reference's PE-{pe} fold")
+                    fails.append(f"pe{pe} {tag}: outside tolerance of the reference's PE-{me} fold")
             if golden is not None:
                 if dt >= 8 and op in (OPS["sum"], OPS["prod"]):
                     tol = oracle.fp_tolerance(dt, op, srcs, ref)
@@ -475,6 +476,95 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             hip.stream_destroy(occ)
             hip.stream_destroy(st)
             for b_ in (ret, d, s):
+                ish.ishmem_free(b_)
+            ish.set_param("max_blocks", int(os.environ.get("ISHMEM_MAX_BLOCKS", 1024)))
+
+        if "stress" in scenarios:
+            # Randomised protocol stress: every iteration draws (same draw on every PE) an
+            # (op, type), a length from 1 element to 4 Mi (log-uniform: granule path, one-shot,
+            # RS + AG with many segments), an element offset, in place or not, a team, a grid
+            # cap per PE, and whether one PE first fills the GPU with an occupying kernel on
+            # another stream (residency perturbation: announce fallback, claims, steals).  The
+            # collectives are chained on one stream with *ret; each window is compared with the
+            # oracle's canonical fold and the guard words around it must be untouched.
+            iters = int(os.environ.get("STRESS_ITERS", 40))
+            seed = int(os.environ.get("STRESS_SEED", 1234))
+            nmax, pad = 4 << 20, 64
+            combos = [(op, dt) for op in range(7) for dt in (DT["int32"], DT["uint64"], DT["float"], DT["double"], DT["uint8"])
+                      if oracle.valid(op, dt)]
+            teams = [(ish.ISHMEM_TEAM_WORLD, list(range(npes)))]
+            if npes >= 3:
+                r_, t_ = ish.ishmem_team_split_strided(ish.ISHMEM_TEAM_WORLD, 0, 2, (npes + 1) // 2)
+                if r_:
+                    fails.append(f"pe{pe} stress split: {ish.last_error()}")
+                else:
+                    teams.append((t_, list(range(0, npes, 2))))
+                r_, t_ = ish.ishmem_team_split_strided(ish.ISHMEM_TEAM_WORLD, 1, 1, npes - 1)
+                if r_:
+                    fails.append(f"pe{pe} stress split: {ish.last_error()}")
+                else:
+                    teams.append((t_, list(range(1, npes))))
+            S = ish.ishmem_malloc((nmax + 2 * pad) * 8)
+            D = ish.ishmem_malloc((nmax + 2 * pad) * 8)
+            ret = ish.ishmem_malloc(4)
+            st, occ = hip.stream_create(), hip.stream_create()
+            cus = int(ish.get_param("cu_count"))
+            done_iters, occupied, kinds = 0, 0, set()
+            for k in range(iters):
+                rng = np.random.default_rng(seed * 7919 + k)
+                op, dt = combos[int(rng.integers(len(combos)))]
+                es = np.dtype(oracle.NP[dt]).itemsize
+                n = int(np.exp(rng.uniform(0.0, np.log(nmax))))
+                n = max(1, min(n, nmax))
+                o = int(rng.integers(0, 4))
+                inplace = bool(rng.random() < 0.25)
+                th, members = teams[int(rng.integers(len(teams)))]
+                occupier = int(rng.integers(npes)) if rng.random() < 0.2 else -1
+                cap = [int(rng.choice([16, 64, 256, 1024])) for _ in range(npes)]
+                tag = (f"stress k={k} op={ONAMES[op]} dt={NAMES[dt]} n={n} o={o} inplace={inplace} "
+                       f"team={members} occ={occupier} cap={cap[pe]}")
+                ish.set_param("max_blocks", cap[pe])
+                lo, hi = (0.5, 2.0) if op == OPS["prod"] else (-1.0, 1.0)
+                ins = [oracle.fill_random(dt, (seed << 20) + k * 64 + j, n, lo, hi) for j in range(len(members))]
+                # Guards: the whole dest region (and the source region in place) holds 0xA5 bytes.
+                hip.memset(D, 0xA5, (nmax + 2 * pad) * 8)
+                hip.synchronize()
+                dbase = D + pad * 8 + o * es
+                sbase = dbase if inplace else S + pad * 8 + o * es
+                if pe in members:
+                    hip.upload(sbase, ins[members.index(pe)])
+                ish.ishmem_barrier_all()
+                if pe == occupier:
+                    ish.occupy(2 * cus, 300, occ)
+                if pe in members:
+                    hip.memset(ret, 0, 4)
+                    r = ish.reduce_on_stream(ONAMES[op], NAMES[dt], dbase, sbase, n, ret, st, th)
+                    hip.stream_synchronize(st)
+                    rv = int(hip.download(ret, 1, np.int32)[0])
+                    if r or rv:
+                        fails.append(f"pe{pe} {tag}: rc={r} ret={rv} {ish.last_error()}")
+                        break
+                    whole = hip.download(D, (nmax + 2 * pad) * 8, np.uint8)
+                    lo_b, hi_b = pad * 8 + o * es, pad * 8 + o * es + n * es
+                    got = whole[lo_b:hi_b].view(oracle.NP[dt])
+                    nf = len(fails)
+                    check(tag, op, dt, ins, got, me=members.index(pe))
+                    if np.any(whole[:lo_b] != 0xA5) or np.any(whole[hi_b:] != 0xA5):
+                        fails.append(f"pe{pe} {tag}: guard bytes around dest overwritten")
+                    if len(fails) > nf:
+                        break
+                hip.stream_synchronize(occ)
+                done_iters += 1
+                kinds.add("ll" if n * es <= 65536 else ("big" if n * es > (1 << 20) else "mid"))
+                occupied += occupier >= 0
+            if pe == 0:
+                print(f"[stress] pe0: {done_iters}/{iters} iterations, {occupied} with an occupier, "
+                      f"sizes {sorted(kinds)}", flush=True)
+            hip.stream_destroy(occ)
+            hip.stream_destroy(st)
+            for th, _m in teams[1:]:
+                ish.ishmem_team_destroy(th)
+            for b_ in (ret, D, S):
                 ish.ishmem_free(b_)
             ish.set_param("max_blocks", int(os.environ.get("ISHMEM_MAX_BLOCKS", 1024)))
 

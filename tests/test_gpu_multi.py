@@ -151,3 +151,12 @@ def test_config5_min_max_prod_int32_f64_4KiB_to_4GiB(npes):
     # chunk edge checked (4 GiB src + 4 GiB dest + staging per PE: a 9 GiB heap).
     run_pes(npes, ["cfg5"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "9G",
                                  "CFG5_MAX_BYTES": 4 << 30}, timeout=900)
+
+
+@pytest.mark.parametrize("npes", [2, 3, 4, 8])
+def test_randomised_protocol_stress(npes):
+    # Random (op, type), lengths 1 .. 4 Mi elements, offsets, in place, teams (world, strided,
+    # shifted), per-PE grid caps and an occupying kernel on a random PE, chained on one stream;
+    # every window vs the oracle's fold, guard bytes around it untouched, *ret clean.
+    # STRESS_ITERS / STRESS_SEED override (longer soak runs).
+    run_pes(npes, ["stress"], env={"ISHMEM_SYMMETRIC_SIZE": "1G"}, timeout=400)
