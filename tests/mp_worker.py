@@ -395,6 +395,111 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             ish.ishmem_free(d)
             ish.ishmem_free(s)
 
+        if "teams2" in scenarios and npes >= 2:
+            # The reference's team tests, restated.
+            W, INV = ish.ISHMEM_TEAM_WORLD, ish.ISHMEM_TEAM_INVALID
+
+            def pat(idx_team, m):  # ((i % (t + 2)) << 16) + i  (team_translate.cpp / team_shared.cpp)
+                i = np.arange(m, dtype=np.int64)
+                return (((i % (idx_team + 2)) << 16) + i).astype(np.int32)
+
+            m = 1 << 10
+            src_b, dst_b = ish.ishmem_malloc(4 * m), ish.ishmem_malloc(4 * m)
+            # (1) test/unit/team_negative_stride.cpp: start npes-1, stride -1, size npes; team
+            # index of world PE k is npes-1-k; fcollect of each PE's id lands reversed.
+            r, rev = ish.ishmem_team_split_strided(W, npes - 1, -1, npes)
+            if r or rev == INV:
+                fails.append(f"pe{pe} split stride -1 rc={r} team={rev} {ish.last_error()}")
+            else:
+                if ish.ishmem_team_translate_pe(W, pe, rev) != npes - 1 - pe:
+                    fails.append(f"pe{pe} stride -1: translate_pe {ish.ishmem_team_translate_pe(W, pe, rev)}")
+                if ish.ishmem_team_my_pe(rev) != npes - 1 - pe or ish.ishmem_team_n_pes(rev) != npes:
+                    fails.append(f"pe{pe} stride -1: team_my_pe / n_pes")
+                hip.upload(src_b, np.array([pe], np.int32))
+                hip.memset(dst_b, 0xFF, 4 * npes)
+                if ish.ishmem_int_fcollect(rev, dst_b, src_b, 1):
+                    fails.append(f"pe{pe} stride -1 fcollect rc {ish.last_error()}")
+                elif not np.array_equal(hip.download(dst_b, npes, np.int32), np.arange(npes - 1, -1, -1)):
+                    fails.append(f"pe{pe} stride -1 fcollect: {hip.download(dst_b, npes, np.int32)}")
+                # FP fold order on the reversed team is ITS team order: world PE npes-1 first.
+                for op, dt, n in ((OPS["sum"], DT["float"], 3001), (OPS["prod"], DT["double"], 777),
+                                  (OPS["max"], DT["int64"], 5000)):
+                    lo, hi = (0.5, 2.0) if op == OPS["prod"] else (-1.0, 1.0)
+                    ins_w = [oracle.fill_random(dt, 0x7E0 + 13 * op + j, n, lo, hi) for j in range(npes)]
+                    s, d = heap(n, dt), heap(n, dt)
+                    hip.upload(s, ins_w[pe])
+                    if ish.reduce(ONAMES[op], NAMES[dt], d, s, n, rev):
+                        fails.append(f"pe{pe} stride -1 reduce rc {ish.last_error()}")
+                    else:
+                        check(f"stride -1 {ONAMES[op]} {NAMES[dt]}", op, dt, ins_w[::-1],
+                              hip.download(d, n, oracle.NP[dt]), me=npes - 1 - pe)
+                    ish.ishmem_free(d)
+                    ish.ishmem_free(s)
+                ish.ishmem_team_destroy(rev)
+            # (2) test/unit/team_translate.cpp: teams of every 2nd and every 3rd PE; my_pe and
+            # translate_pe are -1 exactly off the team; int sum of the per-team-index pattern.
+            r2, t2 = ish.ishmem_team_split_strided(W, 0, 2, (npes - 1) // 2 + 1)
+            r3, t3 = ish.ishmem_team_split_strided(W, 0, 3, (npes - 1) // 3 + 1)
+            if r2 or r3:
+                fails.append(f"pe{pe} translate splits rc={r2},{r3} {ish.last_error()}")
+            p2 = ish.ishmem_team_my_pe(t2) if t2 != INV else -1
+            p3 = ish.ishmem_team_my_pe(t3) if t3 != INV else -1
+            x32 = ish.ishmem_team_translate_pe(t3, p3, t2) if t3 != INV else -1
+            x23 = ish.ishmem_team_translate_pe(t2, p2, t3) if t2 != INV else -1
+            in2, in3 = pe % 2 == 0, pe % 3 == 0
+            want = (p2 != -1, p3 != -1, x23 != -1, x32 != -1)
+            if want != (in2, in3, in2 and in3, in2 and in3):
+                fails.append(f"pe{pe} team_translate: p2={p2} p3={p3} 2->3={x23} 3->2={x32}")
+            if in2 and (p2 != pe // 2 or ish.ishmem_team_translate_pe(W, pe, t2) != p2):
+                fails.append(f"pe{pe} team_translate: world -> team_2s")
+            for tm, tp in ((t2, p2), (t3, p3)):
+                if tm == INV:
+                    continue
+                hip.upload(src_b, pat(tp, m))
+                hip.memset(dst_b, 0, 4 * m)
+                if ish.ishmem_int_sum_reduce(tm, dst_b, src_b, m):
+                    fails.append(f"pe{pe} team_translate reduce rc {ish.last_error()}")
+                    continue
+                ref = sum(pat(j, m).astype(np.int64) for j in range(ish.ishmem_team_n_pes(tm))).astype(np.int32)
+                if not np.array_equal(hip.download(dst_b, m, np.int32), ref):
+                    fails.append(f"pe{pe} team_translate: team reduce wrong")
+            for tm in (t2, t3):
+                if tm != INV:
+                    ish.ishmem_team_destroy(tm)
+            # (3) test/unit/team_shared.cpp: every PE of the node is in ISHMEM_TEAM_SHARED; int sum
+            # over it of the per-world-PE pattern, in-place min of the PE id (the leader, 0), team
+            # size fcollect, then the leader team (stride npes / one member) re-reduces in place.
+            ns = ish.ishmem_team_n_pes(ish.ISHMEM_TEAM_SHARED)
+            if ns != npes or ish.ishmem_team_translate_pe(ish.ISHMEM_TEAM_SHARED, pe, W) != pe:
+                fails.append(f"pe{pe} team_shared: n_pes {ns}")
+            hip.upload(src_b, pat(pe, m))
+            total = sum(pat(j, m).astype(np.int64) for j in range(npes)).astype(np.int32)
+            if ish.ishmem_int_sum_reduce(ish.ISHMEM_TEAM_SHARED, dst_b, src_b, m) or not np.array_equal(
+                    hip.download(dst_b, m, np.int32), total):
+                fails.append(f"pe{pe} team_shared: sum reduce wrong {ish.last_error()}")
+            lead = ish.ishmem_malloc(4)
+            hip.upload(lead, np.array([pe], np.int32))
+            if ish.ishmem_team_sync(ish.ISHMEM_TEAM_SHARED) or ish.ishmem_int_min_reduce(
+                    ish.ISHMEM_TEAM_SHARED, lead, lead, 1) or int(hip.download(lead, 1, np.int32)[0]) != 0:
+                fails.append(f"pe{pe} team_shared: leader min-reduce {ish.last_error()}")
+            hip.upload(src_b + 4 * m - 4, np.array([ns], np.int32))
+            sizes = ish.ishmem_malloc(4 * npes)
+            if ish.ishmem_int_fcollect(sizes, src_b + 4 * m - 4, 1) or not np.all(
+                    hip.download(sizes, npes, np.int32) == ns):
+                fails.append(f"pe{pe} team_shared: size fcollect")
+            r, leaders = ish.ishmem_team_split_strided(W, 0, npes, npes // ns)
+            if r:
+                fails.append(f"pe{pe} team_shared: leader split {ish.last_error()}")
+            elif leaders != INV:
+                if ish.ishmem_int_sum_reduce(leaders, dst_b, dst_b, m) or not np.array_equal(
+                        hip.download(dst_b, m, np.int32), total):
+                    fails.append(f"pe{pe} team_shared: leader reduce wrong")
+                ish.ishmem_team_destroy(leaders)
+            elif pe == 0:
+                fails.append("pe0 team_shared: PE 0 must lead")
+            for b_ in (sizes, lead, dst_b, src_b):
+                ish.ishmem_free(b_)
+
         if "large" in scenarios:
             # f32 sum over 64 Mi elements per PE (256 MiB; 16 Mi beyond 4 PEs, where every
             # process holds all p inputs): full-array comparison.

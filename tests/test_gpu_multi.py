@@ -160,3 +160,13 @@ def test_randomised_protocol_stress(npes):
     # every window vs the oracle's fold, guard bytes around it untouched, *ret clean.
     # STRESS_ITERS / STRESS_SEED override (longer soak runs).
     run_pes(npes, ["stress"], env={"ISHMEM_SYMMETRIC_SIZE": "1G"}, timeout=400)
+
+
+@pytest.mark.parametrize("npes", [2, 3, 6])
+def test_reference_team_tests_negative_stride_translate_shared(npes):
+    # test/unit/team_negative_stride.cpp (reversed team: fcollect order, FP folds in ITS team
+    # order), team_translate.cpp (every-2nd / every-3rd PE teams: my_pe / translate_pe -1 off the
+    # team, int sum of the per-team-index pattern) and team_shared.cpp (SHARED sum, leader
+    # min-reduce in place, size fcollect, leader-team in-place reduce).  6 PEs: PE 0 in both
+    # translate teams, PEs 2 / 4 in one, PE 3 in the other.
+    run_pes(npes, ["teams2"], env={"ISHMEM_MAX_BLOCKS": 16}, timeout=300)
