@@ -162,6 +162,18 @@ def max_over_ranks(dist, vals: list[float]) -> list[float]:
     return [float(x) for x in t]
 
 
+def device_errors(ish) -> float:
+    """Device-side spin timeouts recorded so far on this PE (library error words)."""
+    return float(ish.lib().ishmemi_c_error_count())
+
+
+def legs_healthy(ish, dist) -> bool:
+    """Collective over the ranks: True while no PE has recorded a device timeout.  Once one has,
+    the team's later collectives could each wait out the device timeout, so the remaining GPU legs
+    are skipped on every rank alike and the line already measured is emitted."""
+    return max_over_ranks(dist, [device_errors(ish)])[0] == 0
+
+
 def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max):
     """BASELINE configs[4]: min/max/prod x int32/float64, 4 KiB .. nbytes_max per PE in steps of 4x:
     us per call (max over ranks), algbw, and a check of every word up to 64 MiB, above that of
@@ -192,7 +204,9 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max):
                         raise RuntimeError(ish.last_error())
                 e1.record(stream)
                 hip.stream_synchronize(stream)
-                us = max_over_ranks(dist, [e0.elapsed_ms(e1) * 1000.0 / it])[0]
+                us, errs = max_over_ranks(dist, [e0.elapsed_ms(e1) * 1000.0 / it, device_errors(ish)])
+                if errs:  # every rank sees the same max: all stop here together
+                    raise RuntimeError(f"device timeouts at {op} {dtn} {nb} B: {ish.last_error()}")
                 if nb <= (64 << 20):
                     wins = [(0, n)]
                 else:
@@ -241,7 +255,10 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
                 raise RuntimeError(ish.last_error())
         e1.record(stream)
         hip.stream_synchronize(stream)
-        return max_over_ranks(dist, [e0.elapsed_ms(e1) / iters])[0]
+        ms, errs = max_over_ranks(dist, [e0.elapsed_ms(e1) / iters, device_errors(ish)])
+        if errs:
+            raise RuntimeError(f"device timeouts at {n * 4} B: {ish.last_error()}")
+        return ms
 
     out = []
 
@@ -304,7 +321,9 @@ def xgmi_probe(ish, hip, src, dst, B, world, rank, dist, stream, barrier):
                 raise RuntimeError(ish.last_error())
         e1.record(stream)
         hip.stream_synchronize(stream)
-        ms = max_over_ranks(dist, [e0.elapsed_ms(e1) / k])[0]
+        ms, errs = max_over_ranks(dist, [e0.elapsed_ms(e1) / k, device_errors(ish)])
+        if errs:
+            raise RuntimeError(f"device timeouts in probe {name}: {ish.last_error()}")
         gbs = len(srcs) * S / (ms * 1e-3) / 1e9
         probe[name] = {"bytes_per_peer": S, "peers": len(srcs), "ms": round(ms, 4),
                        "ingress_GBps": round(gbs, 1), "per_link_GBps": round(gbs / len(srcs), 1)}
@@ -559,6 +578,15 @@ def main() -> int:
         targets["met"] = algbw >= 400.0
 
     extra = {}
+    unhealthy = []
+
+    def healthy() -> bool:
+        # Checked before each N>1 GPU leg (collective: same answer on every rank).
+        if not unhealthy and not legs_healthy(ish, dist):
+            unhealthy.append(True)
+            extra["legs_skipped"] = "a PE recorded a device timeout; later GPU legs skipped"
+        return not unhealthy
+
     if world == 1 and not args.no_combine:
         log("combine leg")
         # Local combine unit dst = a + b at the same size (3B HBM bytes per launch).
@@ -579,7 +607,7 @@ def main() -> int:
                             "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("combine2_1pe", B)}
         ish.ishmem_free(b2)
 
-    if world > 1 and not args.no_probe:
+    if world > 1 and healthy() and not args.no_probe:
         log("xGMI probe")
         try:
             probe = xgmi_probe(ish, hip, src, dst, B, world, rank, dist, stream, barrier)
@@ -590,7 +618,7 @@ def main() -> int:
         except Exception as ex:
             extra["xgmi_probe"] = {"error": str(ex)}
 
-    if world > 1 and not args.no_tuning:
+    if world > 1 and healthy() and not args.no_tuning:
         log("launch-shape sweep")
         try:
             extra["xgmi_tuning"] = xgmi_tuning(ish, hip, src, dst, B, world, dist, stream)
@@ -609,7 +637,7 @@ def main() -> int:
     ish.ishmem_free(dst)
     ish.ishmem_free(src)
 
-    if world > 1 and not args.no_tripwire:
+    if world > 1 and healthy() and not args.no_tripwire:
         log("coherence tripwire")
         from ishmem_amd import selfcheck
         try:
@@ -622,7 +650,7 @@ def main() -> int:
         except Exception as ex:
             extra["tripwire"] = {"error": str(ex), "checked": False}
 
-    if world > 1 and not args.no_sweep:
+    if world > 1 and healthy() and not args.no_sweep:
         log("config-5 sweep")
         # BASELINE configs[4] (min/max/prod x int32/float64 across the PEs), 4 KiB .. 4 GiB per PE.
         try:
@@ -630,7 +658,7 @@ def main() -> int:
         except Exception as ex:
             extra["config5_sweep"] = {"error": str(ex)}
 
-    if not args.no_e2e:
+    if not args.no_e2e and (world == 1 or healthy()):
         # Last: its pipeline streams add hardware queues, which oversubscribe the scheduler when
         # several ranks share one GPU (same-device rehearsals) and slow every later leg there.
         log("host-memory end-to-end leg")
