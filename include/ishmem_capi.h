@@ -127,6 +127,13 @@ int ishmemi_c_resync(void);
 int ishmemi_c_reduce(int team, int op, int dtype, void *dest, const void *source, size_t nreduce);
 int ishmemi_c_reduce_on_stream(int team, int op, int dtype, void *dest, const void *source,
                                size_t nreduce, int *ret, void *stream);
+/* The same with the reference's event plumbing: the call runs after every hipEvent_t in
+ * deps[0..ndeps) (its `const std::vector<sycl::event> &deps`, reduce_impl.h:445-453), and, when
+ * `done` (a hipEvent_t) is not NULL, `done` is recorded on `stream` after the call's last launch
+ * (the sycl::event the reference returns, reduce_impl.h:471-472). */
+int ishmemi_c_reduce_on_stream_deps(int team, int op, int dtype, void *dest, const void *source,
+                                    size_t nreduce, int *ret, void *stream, void *const *deps,
+                                    size_t ndeps, void *done);
 
 /* Local combine unit of the path (what one reduce step does per element):
  *   dst[i] = op(srcs[0][i], srcs[1][i], ..., srcs[nsrc-1][i]), folded in source order.

@@ -7,7 +7,9 @@
  * variant below: enqueue on `stream`, return immediately (0 = enqueued); *ret (device-visible
  * int, may be nullptr) is zeroed in stream order at the call's start and set nonzero by any of the
  * call's launches that fails, so it reads 0 after completion exactly when the call succeeded.
- * Dependencies are expressed by stream order / hipStreamWaitEvent instead of `deps`.
+ * The reference's `deps` and returned sycl::event map to the overloads taking
+ * (const hipEvent_t *deps, size_t ndeps, hipEvent_t done): the call waits for every dep and
+ * records `done` (if not NULL) after its last launch.
  */
 #ifndef ISHMEM_AMD_ISHMEMX_H
 #define ISHMEM_AMD_ISHMEMX_H
@@ -20,7 +22,8 @@
  * no reference counterpart — the reference aborts, src/proxy.cpp:79-84). */
 inline int ishmemx_resync(void) { return ishmemi_c_resync(); }
 
-typedef struct ihipStream_t *hipStream_t; /* identical to HIP's own typedef */
+typedef struct ihipStream_t *hipStream_t; /* identical to HIP's own typedefs */
+typedef struct ihipEvent_t *hipEvent_t;
 
 namespace ishmemi_cxx {
 template <typename T>
@@ -29,6 +32,15 @@ inline int reduce_on_stream(ishmem_team_t team, int op, T *dest, const T *source
 {
     return ishmemi_c_reduce_on_stream(team, op, dtype_of<T>(), (void *) dest, (const void *) source,
                                       nreduce, ret, (void *) stream);
+}
+template <typename T>
+inline int reduce_on_stream(ishmem_team_t team, int op, T *dest, const T *source, size_t nreduce,
+                            int *ret, hipStream_t stream, const hipEvent_t *deps, size_t ndeps,
+                            hipEvent_t done)
+{
+    return ishmemi_c_reduce_on_stream_deps(team, op, dtype_of<T>(), (void *) dest,
+                                           (const void *) source, nreduce, ret, (void *) stream,
+                                           (void *const *) deps, ndeps, (void *) done);
 }
 }  // namespace ishmemi_cxx
 
@@ -44,6 +56,21 @@ inline int reduce_on_stream(ishmem_team_t team, int op, T *dest, const T *source
         hipStream_t stream)                                                                        \
     {                                                                                              \
         return ishmemi_cxx::reduce_on_stream<TYPE>(team, OPC, dest, source, nreduce, ret, stream); \
+    }                                                                                              \
+    /* the reference's `deps` / returned event: wait for deps[0..ndeps), then record `done` */     \
+    inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_on_stream(                                   \
+        ishmem_team_t team, TYPE *dest, const TYPE *source, size_t nreduce, int *ret,              \
+        hipStream_t stream, const hipEvent_t *deps, size_t ndeps, hipEvent_t done)                 \
+    {                                                                                              \
+        return ishmemi_cxx::reduce_on_stream<TYPE>(team, OPC, dest, source, nreduce, ret, stream,  \
+                                                   deps, ndeps, done);                             \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_on_stream(                                   \
+        TYPE *dest, const TYPE *source, size_t nreduce, int *ret, hipStream_t stream,              \
+        const hipEvent_t *deps, size_t ndeps, hipEvent_t done)                                     \
+    {                                                                                              \
+        return ishmemi_cxx::reduce_on_stream<TYPE>(ISHMEM_TEAM_WORLD, OPC, dest, source, nreduce,  \
+                                                   ret, stream, deps, ndeps, done);                \
     }
 
 ISHMEMI_CXX_BITWISE_TYPES(ISHMEMI_CXX_ON_STREAM, and, ISHMEMI_OP_AND)

@@ -191,9 +191,21 @@ def reduce(op: str, dtype: str, dest: int, source: int, nreduce: int, team: int 
     return _L.ishmemi_c_reduce(team, OPS[op], DTYPES[dtype], dest, source, nreduce)
 
 
+def _event_handle(e) -> int | None:
+    return getattr(e, "h", e) or None
+
+
 def reduce_on_stream(op: str, dtype: str, dest: int, source: int, nreduce: int, ret: int | None,
-                     stream: int, team: int = ISHMEM_TEAM_WORLD) -> int:
-    """ishmemx_*_reduce_on_queue analogue (src/collectives/reduce_impl.h:444-474)."""
+                     stream: int, team: int = ISHMEM_TEAM_WORLD, deps=(), done=None) -> int:
+    """ishmemx_*_reduce_on_queue analogue (src/collectives/reduce_impl.h:444-474).  `deps`: HIP
+    events (hip.Event or raw handles) the call waits for, as the reference's `deps`; `done`: an
+    event recorded after the call, as the sycl::event the reference returns."""
+    if deps or done is not None:
+        hs = [_event_handle(e) for e in deps]
+        arr = (ctypes.c_void_p * len(hs))(*hs) if hs else None
+        return _L.ishmemi_c_reduce_on_stream_deps(team, OPS[op], DTYPES[dtype], dest, source, nreduce,
+                                                  ret or None, stream or None, arr, len(hs),
+                                                  _event_handle(done))
     return _L.ishmemi_c_reduce_on_stream(team, OPS[op], DTYPES[dtype], dest, source, nreduce,
                                          ret or None, stream or None)
 

@@ -38,6 +38,7 @@ PROTOTYPES = [
     ("ishmemi_c_resync", _i, []),
     ("ishmemi_c_reduce", _i, [_i, _i, _i, _vp, _vp, _sz]),
     ("ishmemi_c_reduce_on_stream", _i, [_i, _i, _i, _vp, _vp, _sz, _vp, _vp]),
+    ("ishmemi_c_reduce_on_stream_deps", _i, [_i, _i, _i, _vp, _vp, _sz, _vp, _vp, _vp, _sz, _vp]),
     ("ishmemi_c_combine", _i, [_i, _i, _vp, ctypes.POINTER(_vp), _i, _sz, _vp]),
     ("ishmemi_c_pull_probe", _i, [_vp, ctypes.POINTER(_vp), _i, _sz, _i, _vp]),
     ("ishmemi_c_occupy", _i, [_i, ctypes.c_ulonglong, _vp]),

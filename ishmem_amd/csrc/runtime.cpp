@@ -1354,6 +1354,25 @@ int ishmemi_c_reduce_on_stream(int team, int op, int dtype, void *dest, const vo
     return reduce_impl(team, op, dtype, dest, source, nreduce, ret, (hipStream_t) stream, false);
 }
 
+int ishmemi_c_reduce_on_stream_deps(int team, int op, int dtype, void *dest, const void *source,
+                                    size_t nreduce, int *ret, void *stream, void *const *deps,
+                                    size_t ndeps, void *done)
+{
+    // The reference's `deps` (set_cmd_grp_dependencies, reduce_impl.h:452-453) become stream
+    // waits ahead of the call's first launch; its returned sycl::event becomes `done`, recorded
+    // after the call's last launch.  Stream order already gives what the reference's per-queue
+    // "last on_queue event" dependency gives on an out-of-order queue.
+    hipStream_t st = (hipStream_t) stream;
+    if (ndeps && !deps) return fail("reduce_on_stream: deps is NULL with ndeps > 0");
+    for (size_t i = 0; i < ndeps; ++i) {
+        if (!deps[i]) return fail("reduce_on_stream: null dependency event");
+        HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t) deps[i], 0));
+    }
+    if (reduce_impl(team, op, dtype, dest, source, nreduce, ret, st, false)) return 1;
+    if (done) HIP_TRY(hipEventRecord((hipEvent_t) done, st));
+    return 0;
+}
+
 int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n,
                       void *stream)
 {

@@ -74,6 +74,11 @@ def memcpy(dst: int, src: int, nbytes: int, kind: int = hipMemcpyDefault) -> Non
                            ctypes.c_int(kind)), "hipMemcpy")
 
 
+def memcpy_async(dst: int, src: int, nbytes: int, stream: int, kind: int = hipMemcpyDefault) -> None:
+    _check(lib().hipMemcpyAsync(ctypes.c_void_p(dst), ctypes.c_void_p(src), ctypes.c_size_t(nbytes),
+                                ctypes.c_int(kind), ctypes.c_void_p(stream)), "hipMemcpyAsync")
+
+
 def memset(dst: int, value: int, nbytes: int) -> None:
     _check(lib().hipMemset(ctypes.c_void_p(dst), ctypes.c_int(value), ctypes.c_size_t(nbytes)), "hipMemset")
 

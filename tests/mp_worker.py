@@ -240,6 +240,27 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 fails.append(f"pe{pe} on_stream rc={r} ret={rv} {ish.last_error()}")
             else:
                 check("on_stream", OPS["sum"], DT["int32"], ins, hip.download(d, n, np.int32))
+            # deps / done (reduce_impl.h:445-472): each PE's source is produced by a copy on
+            # another stream, queued behind a kernel of a PE-dependent length; the reduce waits
+            # for it through `deps` (a missed dependency would fold the zeroed source).
+            ins2 = [oracle.fill_random(DT["int32"], 55 + j, n) for j in range(npes)]
+            hx = hip.host_malloc(n * 4)
+            np.ctypeslib.as_array((np.ctypeslib.ctypes.c_int32 * n).from_address(hx))[:] = ins2[pe]
+            hip.memset(s, 0, n * 4)
+            sa, produced, done = hip.stream_create(), hip.Event(), hip.Event()
+            ish.ishmem_barrier_all()
+            ish.occupy(2, 20_000 * (1 + pe), sa)
+            hip.memcpy_async(s, hx, n * 4, sa)
+            produced.record(sa)
+            r = ish.reduce_on_stream("sum", "int32", d, s, n, ret, st, deps=[produced], done=done)
+            done.synchronize()
+            if r:
+                fails.append(f"pe{pe} on_stream deps rc={r} {ish.last_error()}")
+            else:
+                check("on_stream deps", OPS["sum"], DT["int32"], ins2, hip.download(d, n, np.int32))
+            hip.stream_synchronize(sa)
+            hip.stream_destroy(sa)
+            hip.host_free(hx)
             hip.stream_destroy(st)
             for p in (ret, d, s):
                 ish.ishmem_free(p)

@@ -103,7 +103,10 @@ int main() {
     size_t *z = nullptr;
     int r3 = ishmem_size_and_reduce(z, z, 0);
     int r4 = ishmemx_double_max_reduce_on_stream((double*)nullptr, nullptr, 0, nullptr, nullptr);
-    std::printf("%d %d %d %d %d\n", r1 != 0, r2 != 0, r3 != 0, r4 != 0, ishmem_my_pe());
+    hipEvent_t deps[1] = {nullptr};
+    int r5 = ishmemx_int_sum_reduce_on_stream(ISHMEM_TEAM_WORLD, (int*)nullptr, nullptr, 0, nullptr,
+                                              nullptr, deps, 0, nullptr);  // deps / done overload
+    std::printf("%d %d %d %d %d %d\n", r1 != 0, r2 != 0, r3 != 0, r4 != 0, r5 != 0, ishmem_my_pe());
     return 0;
 }
 ''')
@@ -113,7 +116,7 @@ int main() {
                    check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, out.stderr
-    assert out.stdout.split() == ["1", "1", "1", "1", "-1"]
+    assert out.stdout.split() == ["1", "1", "1", "1", "1", "-1"]
 
 
 def test_c_header_is_plain_c(tmp_path):

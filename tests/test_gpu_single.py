@@ -126,3 +126,40 @@ def test_combine_1GiB_f32_sum_full_compare(ish):
         hip.free(p)
     ish.ishmem_free(d)
     ish.ishmem_free(s)
+
+
+def test_on_stream_deps_and_done_event(ish):
+    """ishmemx_*_reduce_on_queue's `deps` and returned event (reduce_impl.h:445-472) as HIP events:
+    the producer of the source is a copy on ANOTHER stream, queued behind a 100 ms kernel; the
+    reduce on its own stream must wait for it (deps) and `done` must follow the reduce."""
+    from ishmem_amd import hip
+    n = 4 << 20
+    x = oracle.fill_random(oracle.DTYPES["float"], 21, n)
+    hx = hip.host_malloc(n * 4)
+    np.ctypeslib.as_array((np.ctypeslib.ctypes.c_float * n).from_address(hx))[:] = x
+    s, d, ret = ish.ishmem_malloc(n * 4), ish.ishmem_malloc(n * 4), ish.ishmem_malloc(4)
+    hip.memset(s, 0, n * 4)
+    hip.memset(d, 0xFF, n * 4)
+    hip.memset(ret, 0xFF, 4)
+    sa, sb = hip.stream_create(), hip.stream_create()
+    produced, done = hip.Event(), hip.Event()
+    assert ish.occupy(4, 100_000, sa) == 0
+    hip.memcpy_async(s, hx, n * 4, sa)
+    produced.record(sa)
+    assert ish.reduce_on_stream("sum", "float", d, s, n, ret, sb, deps=[produced], done=done) == 0, ish.last_error()
+    done.synchronize()
+    assert _bits_equal(hip.download(d, n, np.float32), x)  # 1 PE: dest = the produced source
+    assert int(hip.download(ret, 1, np.int32)[0]) == 0
+    # `done` alone (no deps), and the NULL-deps error
+    hip.memset(d, 0, n * 4)
+    assert ish.reduce_on_stream("max", "float", d, s, n, None, sb, done=done) == 0
+    done.synchronize()
+    assert _bits_equal(hip.download(d, n, np.float32), x)
+    assert ish.lib().ishmemi_c_reduce_on_stream_deps(0, 4, 8, d, s, n, None, sb, None, 2, None) != 0
+    assert "deps" in ish.last_error()
+    hip.stream_synchronize(sa)
+    for st in (sa, sb):
+        hip.stream_destroy(st)
+    for p in (ret, d, s):
+        ish.ishmem_free(p)
+    hip.host_free(hx)
