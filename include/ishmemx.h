@@ -44,6 +44,40 @@ inline int reduce_on_stream(ishmem_team_t team, int op, T *dest, const T *source
 }
 }  // namespace ishmemi_cxx
 
+/* Generic forms, as the reference's template <typename T> ishmemx_<op>_reduce_on_queue
+ * (src/ishmemx.h:1173, :1191 and the same for every op). */
+#define ISHMEMI_CXX_GENERIC_ON_STREAM(OPNAME, OPC)                                                  \
+    template <typename T>                                                                          \
+    inline int ishmemx_##OPNAME##_reduce_on_stream(T *dest, const T *source, size_t nreduce,        \
+                                                   int *ret, hipStream_t stream)                   \
+    {                                                                                              \
+        return ishmemi_cxx::reduce_on_stream<T>(ISHMEM_TEAM_WORLD, OPC, dest, source, nreduce, ret, \
+                                                stream);                                           \
+    }                                                                                              \
+    template <typename T>                                                                          \
+    inline int ishmemx_##OPNAME##_reduce_on_stream(ishmem_team_t team, T *dest, const T *source,    \
+                                                   size_t nreduce, int *ret, hipStream_t stream)   \
+    {                                                                                              \
+        return ishmemi_cxx::reduce_on_stream<T>(team, OPC, dest, source, nreduce, ret, stream);     \
+    }                                                                                              \
+    template <typename T>                                                                          \
+    inline int ishmemx_##OPNAME##_reduce_on_stream(ishmem_team_t team, T *dest, const T *source,    \
+                                                   size_t nreduce, int *ret, hipStream_t stream,   \
+                                                   const hipEvent_t *deps, size_t ndeps,           \
+                                                   hipEvent_t done)                                \
+    {                                                                                              \
+        return ishmemi_cxx::reduce_on_stream<T>(team, OPC, dest, source, nreduce, ret, stream,      \
+                                                deps, ndeps, done);                                \
+    }
+
+ISHMEMI_CXX_GENERIC_ON_STREAM(and, ISHMEMI_OP_AND)
+ISHMEMI_CXX_GENERIC_ON_STREAM(or, ISHMEMI_OP_OR)
+ISHMEMI_CXX_GENERIC_ON_STREAM(xor, ISHMEMI_OP_XOR)
+ISHMEMI_CXX_GENERIC_ON_STREAM(max, ISHMEMI_OP_MAX)
+ISHMEMI_CXX_GENERIC_ON_STREAM(min, ISHMEMI_OP_MIN)
+ISHMEMI_CXX_GENERIC_ON_STREAM(sum, ISHMEMI_OP_SUM)
+ISHMEMI_CXX_GENERIC_ON_STREAM(prod, ISHMEMI_OP_PROD)
+
 #define ISHMEMI_CXX_ON_STREAM(TYPENAME, TYPE, OPNAME, OPC)                                          \
     inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_on_stream(                                   \
         TYPE *dest, const TYPE *source, size_t nreduce, int *ret, hipStream_t stream)              \
