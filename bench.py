@@ -498,6 +498,8 @@ def main() -> int:
     # overheads of the multi-PE path on a one-GPU box.  Never used for reported numbers.
     device = 0 if same_device else local_rank
     ish.init(rank, world, device, key)
+    # Memory kind the PEs agreed on for the flag rows peers store into (runtime.cpp FlagMem).
+    flag_memory = ("uncached", "fine-grained", "coarse-grained")[int(ish.get_param("flags_kind"))]
     src = ish.ishmem_malloc(B)
     dst = ish.ishmem_malloc(B)
     if not (src and dst):
@@ -713,6 +715,7 @@ def main() -> int:
                        "bytes_per_pe": B, "pes": world,
                        "parallelism": "1 PE self-reduce" if world == 1 else f"direct RS+AG over {world} PEs"},
             "kernel_ms": kern_ms, "checked": checked, "targets": targets,
+            **({"flag_memory": flag_memory} if world > 1 else {}),
             **({"dev_same_device": True} if same_device else {}), "roofline": roof,
             "cpu_baseline": cpu, **extra,
         }

@@ -87,7 +87,7 @@ struct Team {
 };
 
 struct PeRecord {
-    int32_t pe, pid, device, flags_fine_grained;
+    int32_t pe, pid, device, flags_kind;
     char pci_bus[32];  // identifies the physical GPU across processes
     uint64_t heap_size;
     // Launch-shape parameters: the multi-PE kernels pair workgroup b with workgroup b of every
@@ -110,8 +110,8 @@ struct State {
     std::map<size_t, size_t> used;       // offset -> bytes
     char *peer_heap[kMaxPes] = {};
 
-    uint32_t *flags = nullptr;  // kMaxTeams flag blocks, fine-grained device memory
-    bool flags_fine_grained = false;
+    uint32_t *flags = nullptr;  // kMaxTeams flag blocks (+ LL rings), see FlagMem
+    int flags_kind = 0;         // FlagMem of the block in use
     uint32_t *peer_flags[kMaxPes] = {};
     uint32_t *err_host = nullptr;  // host-mapped error words, one per team (+1: device API)
     uint32_t *err_dev = nullptr;
@@ -770,6 +770,51 @@ int sync_device_ctx(State &s)
     return 0;
 }
 
+// Memory of the flag block (start / ready / done rows and the LL rings), which peers store into
+// over xGMI while this PE's kernels poll it.  Best first:
+//   uncached VRAM      every access goes to HBM, so a peer's store is seen by the next poll;
+//   fine-grained VRAM  coherent device memory (hipDeviceMallocFinegrained);
+//   coarse-grained     plain hipMalloc: polls are system-scope loads, but a line of local
+//                      coarse-grained memory may stay in this device's L2 while a peer on another
+//                      device writes HBM behind it — safe only when the PEs share one device.
+enum FlagMem { kFlagsUncached = 0, kFlagsFineGrained = 1, kFlagsCoarse = 2, kFlagKinds = 3 };
+
+const char *flag_kind_name(int k)
+{
+    return k == kFlagsUncached ? "uncached" : k == kFlagsFineGrained ? "fine-grained" : "coarse-grained";
+}
+
+// Allocates (zeroed) a flag block of the first kind >= `kind` that this device can allocate AND
+// export over IPC; the kind used is stored in s.flags_kind.  Returns nonzero if none can.
+int alloc_flags(State &s, int kind, bool exportable, hipIpcMemHandle_t *h)
+{
+    const size_t bytes = kFlagAllocBytes;
+    for (int k = kind; k < kFlagKinds; ++k) {
+        uint32_t *f = nullptr;
+        hipError_t e = k == kFlagsUncached ? hipExtMallocWithFlags((void **) &f, bytes, hipDeviceMallocUncached)
+                       : k == kFlagsFineGrained
+                           ? hipExtMallocWithFlags((void **) &f, bytes, hipDeviceMallocFinegrained)
+                           : hipMalloc((void **) &f, bytes);
+        if (e != hipSuccess) {
+            (void) hipGetLastError();
+            continue;
+        }
+        if (exportable && hipIpcGetMemHandle(h, f) != hipSuccess) {
+            (void) hipGetLastError();
+            (void) hipFree(f);
+            continue;
+        }
+        if (hipMemset(f, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void) hipFree(f);
+            return fail("init: flag block memset failed");
+        }
+        s.flags = f;
+        s.flags_kind = k;
+        return 0;
+    }
+    return fail("init: no flag-block memory kind could be allocated and exported");
+}
+
 int init_impl(int pe, int npes, int device, const std::string &key)
 {
     State &s = S();
@@ -805,16 +850,11 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.used.clear();
     s.free_list[0] = s.heap_size;
 
-    // Barrier flags: fine-grained (uncached) device memory, written by peers over xGMI.
-    const size_t flag_bytes = kFlagAllocBytes;
-    if (hipExtMallocWithFlags((void **) &s.flags, flag_bytes, hipDeviceMallocUncached) == hipSuccess) {
-        s.flags_fine_grained = true;
-    } else {
-        (void) hipGetLastError();
-        HIP_TRY(hipMalloc((void **) &s.flags, flag_bytes));
-        s.flags_fine_grained = false;
-    }
-    HIP_TRY(hipMemset(s.flags, 0, flag_bytes));
+    // Barrier flags (written by peers over xGMI): the best memory kind that can also be exported.
+    // ISHMEM_FLAGS_KIND (tests): start the ladder at FlagMem 1 or 2 instead of uncached VRAM.
+    hipIpcMemHandle_t flags_handle{};
+    const int first_kind = (int) std::min<long long>(kFlagsCoarse, std::max<long long>(0, env_ll("ISHMEM_FLAGS_KIND", 0)));
+    if (alloc_flags(s, first_kind, npes > 1, &flags_handle)) return 1;
     HIP_TRY(hipHostMalloc((void **) &s.err_host, (kMaxTeams + 1) * sizeof(uint32_t),
                           hipHostMallocMapped | hipHostMallocCoherent));
     memset(s.err_host, 0, (kMaxTeams + 1) * sizeof(uint32_t));
@@ -842,7 +882,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.pe = pe;
         mine.pid = (int32_t) getpid();
         mine.device = s.device;
-        mine.flags_fine_grained = s.flags_fine_grained ? 1 : 0;
+        mine.flags_kind = s.flags_kind;
         mine.heap_size = s.heap_size;
         mine.max_blocks = s.max_blocks;
         mine.ll_max_bytes = s.ll_max_bytes;
@@ -853,19 +893,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             snprintf(mine.pci_bus, sizeof(mine.pci_bus), "dev%d", s.device);
         }
         HIP_TRY(hipIpcGetMemHandle(&mine.heap_handle, s.heap));
-        if (hipIpcGetMemHandle(&mine.flags_handle, s.flags) != hipSuccess) {
-            // Uncached allocations that cannot be exported: fall back to coarse-grained flags
-            // (every flag access is a system-scope atomic, so correctness does not depend on it).
-            (void) hipGetLastError();
-            (void) hipFree(s.flags);
-            HIP_TRY(hipMalloc((void **) &s.flags, flag_bytes));
-            HIP_TRY(hipMemset(s.flags, 0, flag_bytes));
-            HIP_TRY(hipDeviceSynchronize());
-            s.flags_fine_grained = false;
-            s.peer_flags[pe] = s.flags;
-            mine.flags_fine_grained = 0;
-            HIP_TRY(hipIpcGetMemHandle(&mine.flags_handle, s.flags));
-        }
+        mine.flags_handle = flags_handle;
         PeRecord all[kMaxPes];
         if (s.boot.allgather(&mine, all, sizeof(PeRecord), err)) return fail(err);
         // Agree on the parameters that choose a call's kernel (the minimum over the PEs), so a
@@ -900,43 +928,61 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_heap[j], all[j].heap_handle,
                                         hipIpcMemLazyEnablePeerAccess));
         }
-        // Flags (+ LL rings): if any PE cannot import a peer's fine-grained export, every PE
-        // re-exports a coarse-grained block instead (every flag and granule access is a
-        // system-scope atomic, so the protocol does not depend on the memory type).
-        int32_t opened = 1;
-        for (int j = 0; j < npes && opened; ++j) {
-            if (j == pe) continue;
-            if (hipIpcOpenMemHandle((void **) &s.peer_flags[j], all[j].flags_handle,
-                                    hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-                (void) hipGetLastError();
-                s.peer_flags[j] = nullptr;
-                opened = 0;
+        // Flags (+ LL rings): every PE uses the same memory kind, the least capable one any PE
+        // could allocate and export; if some PE cannot import a peer's block of that kind, all
+        // step down one kind together and exchange new blocks.
+        int kind = 0;
+        bool fresh = false;  // identical on every PE: all take the same branches below
+        for (int j = 0; j < npes; ++j) kind = std::max(kind, (int) all[j].flags_kind);
+        for (int j = 0; j < npes; ++j) fresh = fresh || all[j].flags_kind != kind;
+        hipIpcMemHandle_t hs[kMaxPes];
+        for (int j = 0; j < npes; ++j) hs[j] = all[j].flags_handle;
+        for (;;) {
+            if (fresh) {
+                // Every PE replaces its block by one of `kind` (or the next kind it can make).
+                if (s.boot.barrier(err)) return fail(err);  // no peer still maps our old block
+                (void) hipFree(s.flags);
+                s.flags = nullptr;
+                hipIpcMemHandle_t h{};
+                if (alloc_flags(s, kind, true, &h)) return 1;
+                s.peer_flags[pe] = s.flags;
+                int32_t k = s.flags_kind, ks[kMaxPes];
+                if (s.boot.allgather(&k, ks, sizeof(k), err)) return fail(err);
+                if (s.boot.allgather(&h, hs, sizeof(h), err)) return fail(err);
+                int agreed = kind;
+                for (int j = 0; j < npes; ++j) agreed = std::max(agreed, (int) ks[j]);
+                fresh = false;
+                for (int j = 0; j < npes; ++j) fresh = fresh || ks[j] != agreed;
+                kind = agreed;
+                if (fresh) continue;  // PEs ended on different kinds: again, at the lesser one
             }
-        }
-        int32_t all_opened[kMaxPes];
-        if (s.boot.allgather(&opened, all_opened, sizeof(int32_t), err)) return fail(err);
-        bool retry = false;
-        for (int j = 0; j < npes; ++j) retry = retry || !all_opened[j];
-        if (retry) {
+            int32_t opened = 1;
+            for (int j = 0; j < npes && opened; ++j) {
+                if (j == pe) continue;
+                if (hipIpcOpenMemHandle((void **) &s.peer_flags[j], hs[j], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                    (void) hipGetLastError();
+                    s.peer_flags[j] = nullptr;
+                    opened = 0;
+                }
+            }
+            int32_t all_opened[kMaxPes];
+            if (s.boot.allgather(&opened, all_opened, sizeof(int32_t), err)) return fail(err);
+            bool ok = true;
+            for (int j = 0; j < npes; ++j) ok = ok && all_opened[j];
+            if (ok) break;
             for (int j = 0; j < npes; ++j) {
                 if (j != pe && s.peer_flags[j]) (void) hipIpcCloseMemHandle(s.peer_flags[j]);
                 s.peer_flags[j] = nullptr;
             }
-            if (s.boot.barrier(err)) return fail(err);  // no peer still maps our old block
-            (void) hipFree(s.flags);
-            HIP_TRY(hipMalloc((void **) &s.flags, flag_bytes));
-            HIP_TRY(hipMemset(s.flags, 0, flag_bytes));
-            HIP_TRY(hipDeviceSynchronize());
-            s.flags_fine_grained = false;
             s.peer_flags[pe] = s.flags;
-            hipIpcMemHandle_t h, hs[kMaxPes];
-            HIP_TRY(hipIpcGetMemHandle(&h, s.flags));
-            if (s.boot.allgather(&h, hs, sizeof(h), err)) return fail(err);
-            for (int j = 0; j < npes; ++j) {
-                if (j == pe) continue;
-                HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_flags[j], hs[j], hipIpcMemLazyEnablePeerAccess));
-            }
+            if (++kind >= kFlagKinds) return fail("init: no flag-block memory kind can be imported by every PE");
+            fresh = true;
         }
+        if (s.flags_kind == kFlagsCoarse && share < npes)
+            fprintf(stderr,
+                    "ishmem_amd: PE %d: flag block is coarse-grained device memory while PEs span "
+                    "several devices; peers' flag stores may stay invisible to this device's polls "
+                    "(device timeouts). Uncached / fine-grained VRAM could not be shared.\n", pe);
         if (s.boot.barrier(err)) return fail(err);  // every peer has imported our handles
     }
 
@@ -1500,7 +1546,8 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "oneshot_p2_max_bytes") return s.oneshot_p2;
     if (n == "ll_max_bytes") return s.ll_max_bytes;
     if (n == "debug") return s.debug;
-    if (n == "flags_fine_grained") return s.flags_fine_grained ? 1 : 0;
+    if (n == "flags_fine_grained") return s.flags_kind != kFlagsCoarse ? 1 : 0;
+    if (n == "flags_kind") return s.flags_kind;
     if (n == "staging_bytes") return (long long) s.staging_bytes;
     if (n == "heap_bytes") return (long long) s.heap_size;
     if (n == "launch_words") return (long long) (uintptr_t) s.kern_ep;  // debug: device address

@@ -91,6 +91,11 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 elif not _bits_equal(golden, got):
                     fails.append(f"pe{pe} {tag}: differs from MPICH golden")
 
+        if "flagkind" in scenarios:
+            want = int(os.environ["FLAGKIND_WANT"])
+            if int(ish.get_param("flags_kind")) != want:
+                fails.append(f"pe{pe} flags_kind {ish.get_param('flags_kind')} != agreed {want}")
+
         if "timeout" in scenarios:
             # Failure detection: PE 0 enters collectives PE 1 never joins.  Every device-side
             # spin is bounded, so the call returns nonzero with a diagnostic instead of hanging

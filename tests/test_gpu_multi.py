@@ -170,3 +170,12 @@ def test_reference_team_tests_negative_stride_translate_shared(npes):
     # min-reduce in place, size fcollect, leader-team in-place reduce).  6 PEs: PE 0 in both
     # translate teams, PEs 2 / 4 in one, PE 3 in the other.
     run_pes(npes, ["teams2"], env={"ISHMEM_MAX_BLOCKS": 16}, timeout=300)
+
+
+@pytest.mark.parametrize("kinds", [[0, 1], [1, 1], [2, 2], [0, 2, 1]])
+def test_flag_memory_kinds_agree_and_work(kinds):
+    # The flag block's memory kind (uncached / fine-grained / coarse-grained VRAM) is agreed at
+    # init: every PE ends on the least capable kind any PE starts from (ISHMEM_FLAGS_KIND per PE),
+    # and the collectives (LL, RS + AG, fcollect, scan) work on each kind.
+    run_pes(len(kinds), ["flagkind", "inplace", "edge", "stream"],
+            env={"ISHMEM_FLAGS_KIND": kinds, "FLAGKIND_WANT": max(kinds)})
