@@ -198,6 +198,26 @@ __global__ __launch_bounds__(BS) void ldsdma_copy(const f4 *__restrict__ a, cons
     }
 }
 
+// Copy with a second, far item per thread: items i and i + n/2 (two DRAM regions in flight per
+// wave), nt loads, write-through stores.
+template <int BS>
+__global__ __launch_bounds__(BS) void split_halves(const f4 *__restrict__ a, const f4 *__restrict__ b,
+                                                   f4 *__restrict__ d, long n)
+{
+    const long h = n / 2;
+    const long i = (long) blockIdx.x * BS + threadIdx.x;
+    const __amdgpu_buffer_rsrc_t r0 =
+        __builtin_amdgcn_make_buffer_rsrc((void *) (d + (long) blockIdx.x * BS), (short) 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r1 =
+        __builtin_amdgcn_make_buffer_rsrc((void *) (d + h + (long) blockIdx.x * BS), (short) 0, 0x7FFFFFFF, 0x00020000);
+    if (i < h) {
+        const f4 x = __builtin_nontemporal_load(a + i);
+        const f4 y = __builtin_nontemporal_load(a + h + i);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x), r0, threadIdx.x * 16, 0, 17);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), r1, threadIdx.x * 16, 0, 17);
+    }
+}
+
 struct Variant {
     std::string name;
     void (*launch)(const f4 *, const f4 *, f4 *, long, int, hipStream_t);
@@ -254,6 +274,21 @@ void OA(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
 {
     const long g = (n + BS - 1) / BS;
     hipLaunchKernelGGL((oneshot_aux<NSRC, BS, LAUX, SAUX>), dim3(g), dim3(BS), 0, s, a, b, d, n);
+}
+
+// The product copy shape with `lds` bytes of dynamic LDS per workgroup: caps workgroups (waves)
+// per CU, i.e. requests in flight per CU.
+template <int NSRC, int BS, int LAUX, int SAUX, int LDS>
+void OAL(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
+{
+    const long g = (n + BS - 1) / BS;
+    hipLaunchKernelGGL((oneshot_aux<NSRC, BS, LAUX, SAUX>), dim3(g), dim3(BS), LDS, s, a, b, d, n);
+}
+template <int BS>
+void SH(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
+{
+    const long g = (n / 2 + BS - 1) / BS;
+    hipLaunchKernelGGL((split_halves<BS>), dim3(g), dim3(BS), 0, s, a, b, d, n);
 }
 
 void MC(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
@@ -344,6 +379,18 @@ int main(int argc, char **argv)
     vs.push_back({"writeonly U1 plain (traffic=1B)", WO<1, 256, false>, 0, 0});
     vs.push_back({"writeonly U1 nt (traffic=1B)", WO<1, 256, true>, 0, 0});
     vs.push_back({"readonly U1 nt (traffic=1B)", RO<1, 256, true>, 0, 0});
+    }
+    if (set == "r2") {  // round 2: requests in flight per CU, and two DRAM regions per wave
+        vs.push_back({"aux ns1 bs64 ld nt / st sc0sc1 (product)", OA<1, 64, 2, 17>, 0, 1});
+        vs.push_back({"  + 4 KiB LDS (<=40 wg/CU)", OAL<1, 64, 2, 17, 4096>, 0, 1});
+        vs.push_back({"  + 8 KiB LDS (<=20 wg/CU)", OAL<1, 64, 2, 17, 8192>, 0, 1});
+        vs.push_back({"  + 16 KiB LDS (<=10 wg/CU)", OAL<1, 64, 2, 17, 16384>, 0, 1});
+        vs.push_back({"  + 32 KiB LDS (<=5 wg/CU)", OAL<1, 64, 2, 17, 32768>, 0, 1});
+        vs.push_back({"split halves bs64 nt / sc0sc1", SH<64>, 0, 1});
+        vs.push_back({"split halves bs128 nt / sc0sc1", SH<128>, 0, 1});
+        vs.push_back({"aux ns2 bs64 ld nt / st sc0sc1 (product a+b)", OA<2, 64, 2, 17>, 0, 2});
+        vs.push_back({"  a+b + 8 KiB LDS", OAL<2, 64, 2, 17, 8192>, 0, 2});
+        vs.push_back({"  a+b + 16 KiB LDS", OAL<2, 64, 2, 17, 16384>, 0, 2});
     }
     hipStream_t s;
     CK(hipStreamCreate(&s));
