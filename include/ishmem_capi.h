@@ -152,6 +152,10 @@ int ishmemi_c_pull_probe(void *dst, const void *const *srcs, int nsrc, size_t nb
  * each hold half a CU (1024 work-items, 80 KiB of LDS) for `usec` microseconds (<= 60 s), so a
  * test can run collectives while another kernel holds most CUs. */
 int ishmemi_c_occupy(int grid, unsigned long long usec, void *stream);
+/* Test hook (no reference counterpart): dst[i] = a[i] + b[i] over n uint32 with ordinary loads and
+ * stores, like a user's producer kernel (its results may still be dirty in this device's L2 when
+ * the next kernel starts).  Asynchronous on `stream`; 4-B aligned pointers. */
+int ishmemi_c_produce_u32(void *dst, const void *a, const void *b, size_t n, void *stream);
 
 /* ---- the collectives next to the reduce, same machinery -------------
  * fcollect: dest[j*nbytes ..] = member j's source, in team order, on every member

@@ -42,6 +42,7 @@ PROTOTYPES = [
     ("ishmemi_c_combine", _i, [_i, _i, _vp, ctypes.POINTER(_vp), _i, _sz, _vp]),
     ("ishmemi_c_pull_probe", _i, [_vp, ctypes.POINTER(_vp), _i, _sz, _i, _vp]),
     ("ishmemi_c_occupy", _i, [_i, ctypes.c_ulonglong, _vp]),
+    ("ishmemi_c_produce_u32", _i, [_vp, _vp, _vp, _sz, _vp]),
     ("ishmemi_c_fcollect", _i, [_i, _vp, _vp, _sz]),
     ("ishmemi_c_fcollect_on_stream", _i, [_i, _vp, _vp, _sz, _vp, _vp]),
     ("ishmemi_c_collect", _i, [_i, _vp, _vp, _sz]),

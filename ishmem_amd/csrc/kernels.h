@@ -162,5 +162,6 @@ void set_device_share(int share);
 int device_share();
 // Test hook: `grid` workgroups that each hold half a CU (1024 work-items, 80 KiB LDS) for `usec`.
 hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s);
+hipError_t launch_produce_u32(uint32_t *dst, const uint32_t *a, const uint32_t *b, uint64_t n, hipStream_t s);
 
 }  // namespace ishmemi

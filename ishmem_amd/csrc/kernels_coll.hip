@@ -232,6 +232,18 @@ __global__ __launch_bounds__(kOccupyThreads) void occupy_kernel(uint64_t ticks, 
     if (sink && lds[(threadIdx.x * 17) % kOccupyLdsWords] == 0xFFFFFFFFu) *sink = 1;  // keeps LDS live
 }
 
+// Test hook (ishmemi_c_produce_u32): dst[i] = a[i] + b[i] over uint32 with ORDINARY loads and
+// stores — what a user's producer kernel does — so its results may sit dirty in this device's L2
+// when the next kernel on the stream (a collective) starts.  The coherence tripwire uses it
+// instead of the library's write-through combine, so a peer reading stale HBM under dirty L2
+// lines would show.
+__global__ __launch_bounds__(256) void produce_u32_kernel(uint32_t *__restrict__ dst, const uint32_t *__restrict__ a,
+                                                          const uint32_t *__restrict__ b, uint64_t n)
+{
+    for (uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t) gridDim.x * 256)
+        dst[i] = a[i] + b[i];
+}
+
 template <typename K, typename A>
 hipError_t launch_res(K kernel, const A &a, int grid, hipStream_t s)
 {
@@ -253,6 +265,14 @@ hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s)
 {
     if (grid < 1 || usec > 60ull * 1000 * 1000) return hipErrorInvalidValue;
     hipLaunchKernelGGL(occupy_kernel, dim3(grid), dim3(kOccupyThreads), 0, s, usec * 100ull, (uint32_t *) nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_produce_u32(uint32_t *dst, const uint32_t *a, const uint32_t *b, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const uint64_t g = std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(produce_u32_kernel, dim3((unsigned) g), dim3(256), 0, s, dst, a, b, n);
     return hipGetLastError();
 }
 

@@ -1460,6 +1460,14 @@ int ishmemi_c_pull_probe(void *dst, const void *const *srcs, int nsrc, size_t nb
     return 0;
 }
 
+int ishmemi_c_produce_u32(void *dst, const void *a, const void *b, size_t n, void *stream)
+{
+    if (n && (!dst || !a || !b)) return fail("produce_u32: null pointer");
+    if (((uintptr_t) dst | (uintptr_t) a | (uintptr_t) b) & 3) return fail("produce_u32: misaligned pointer");
+    HIP_TRY(launch_produce_u32((uint32_t *) dst, (const uint32_t *) a, (const uint32_t *) b, n, (hipStream_t) stream));
+    return 0;
+}
+
 int ishmemi_c_occupy(int grid, unsigned long long usec, void *stream)
 {
     HIP_TRY(launch_occupy(grid, (uint64_t) usec, (hipStream_t) stream));

@@ -3,8 +3,8 @@ tests).  Everything runs through the C-ABI; the expected values come from a host
 every PE's state in wrapping int32 arithmetic, so every checked word is exact.
 
 Each iteration k, on one stream, with no host synchronisation between producer and collective:
-  1. a producer kernel (the library's local combine) rewrites this PE's source window from the
-     previous iteration's dest: S[o:o+n] = D[o:o+n] + base_pe[:n];
+  1. a producer kernel with ORDINARY (write-back) stores, like a user's, rewrites this PE's
+     source window from the previous iteration's dest: S[o:o+n] = D[o:o+n] + base_pe[:n];
   2. ishmemx_int32_sum_reduce_on_stream(D + o, S + o, n) over team T_k.
 The window offset o (0..3 elements: aligned and misaligned heads/tails), the length n (large
 windows for reduce-scatter + all-gather, every fourth one small enough for the one-hop granule
@@ -62,7 +62,7 @@ def chain_tripwire(ish, hip, pe: int, npes: int, nmax: int = 1 << 20, iters: int
             n = small + k if k % 4 == 3 else nmax - 3 * k
             th, members = teams[k % 2]
             if pe in members:
-                if ish.combine("sum", "uint32", S + 4 * o, [D + 4 * o, B], n, st) != 0:
+                if ish.lib().ishmemi_c_produce_u32(S + 4 * o, D + 4 * o, B, n, st) != 0:
                     raise RuntimeError(f"tripwire: producer failed: {ish.last_error()}")
                 if ish.reduce_on_stream("sum", "int32", D + 4 * o, S + 4 * o, n, None, st, th) != 0:
                     raise RuntimeError(f"tripwire: reduce failed: {ish.last_error()}")
