@@ -170,6 +170,11 @@ int ishmemi_c_fcollect(int team, void *dest, const void *source, size_t nbytes);
 int ishmemi_c_fcollect_on_stream(int team, void *dest, const void *source, size_t nbytes, int *ret,
                                  void *stream);
 int ishmemi_c_collect(int team, void *dest, const void *source, size_t nbytes);
+/* collect enqueued on `stream` (ishmemx_<TN>_collect_on_queue, src/ishmemx.h): the members'
+ * byte counts are exchanged on the device inside the launch, so the call returns at once.  *ret as
+ * for ishmemi_c_reduce_on_stream.  dest and (non-empty) source: symmetric-heap memory. */
+int ishmemi_c_collect_on_stream(int team, void *dest, const void *source, size_t nbytes, int *ret,
+                                void *stream);
 int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *source, size_t nelems);
 int ishmemi_c_scan_on_stream(int team, int dtype, int inclusive, void *dest, const void *source,
                              size_t nelems, int *ret, void *stream);

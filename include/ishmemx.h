@@ -115,7 +115,7 @@ ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, min, ISHMEMI_OP_MIN)
 ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, sum, ISHMEMI_OP_SUM)
 ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_ON_STREAM, prod, ISHMEMI_OP_PROD)
 
-/* fcollect / scan on a stream (src/ishmemx.h fcollect/inscan/exscan _on_queue). */
+/* fcollect / collect / scan on a stream (src/ishmemx.h fcollect/collect/inscan/exscan _on_queue). */
 inline int ishmemx_fcollectmem_on_stream(ishmem_team_t team, void *dest, const void *source,
                                          size_t nbytes, int *ret, hipStream_t stream)
 {
@@ -125,6 +125,18 @@ inline int ishmemx_fcollectmem_on_stream(void *dest, const void *source, size_t 
                                          hipStream_t stream)
 {
     return ishmemx_fcollectmem_on_stream(ISHMEM_TEAM_WORLD, dest, source, nbytes, ret, stream);
+}
+
+/* collect with per-PE counts on a stream (src/ishmemx.h collectmem / <TN>_collect _on_queue). */
+inline int ishmemx_collectmem_on_stream(ishmem_team_t team, void *dest, const void *source,
+                                        size_t nbytes, int *ret, hipStream_t stream)
+{
+    return ishmemi_c_collect_on_stream(team, dest, source, nbytes, ret, (void *) stream);
+}
+inline int ishmemx_collectmem_on_stream(void *dest, const void *source, size_t nbytes, int *ret,
+                                        hipStream_t stream)
+{
+    return ishmemx_collectmem_on_stream(ISHMEM_TEAM_WORLD, dest, source, nbytes, ret, stream);
 }
 
 #define ISHMEMI_CXX_COLL_ON_STREAM(TYPENAME, TYPE, UNUSED1, UNUSED2)                                 \
@@ -140,6 +152,19 @@ inline int ishmemx_fcollectmem_on_stream(void *dest, const void *source, size_t 
     {                                                                                              \
         return ishmemx_##TYPENAME##_fcollect_on_stream(ISHMEM_TEAM_WORLD, dest, source, nelems,    \
                                                        ret, stream);                               \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_collect_on_stream(ishmem_team_t team, TYPE *dest,               \
+                                                      const TYPE *source, size_t nelems, int *ret,  \
+                                                      hipStream_t stream)                           \
+    {                                                                                              \
+        return ishmemi_c_collect_on_stream(team, (void *) dest, (const void *) source,              \
+                                           nelems * sizeof(TYPE), ret, (void *) stream);            \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_collect_on_stream(TYPE *dest, const TYPE *source, size_t nelems, \
+                                                      int *ret, hipStream_t stream)                 \
+    {                                                                                              \
+        return ishmemx_##TYPENAME##_collect_on_stream(ISHMEM_TEAM_WORLD, dest, source, nelems, ret, \
+                                                      stream);                                     \
     }                                                                                              \
     inline int ishmemx_##TYPENAME##_sum_inscan_on_stream(ishmem_team_t team, TYPE *dest,            \
                                                          const TYPE *source, size_t nelems,         \

@@ -266,6 +266,12 @@ def ishmem_collectmem(*args) -> int:
     return _L.ishmemi_c_collect(team, dest, source, n)
 
 
+def collect_on_stream(dest: int, source: int, nbytes: int, ret: int | None, stream: int,
+                      team: int = ISHMEM_TEAM_WORLD) -> int:
+    """ishmemx_collectmem_on_queue analogue: nbytes may differ per PE; counts meet on the device."""
+    return _L.ishmemi_c_collect_on_stream(team, dest, source, nbytes, ret or None, stream or None)
+
+
 def fcollect_on_stream(dest: int, source: int, nbytes: int, ret: int | None, stream: int,
                        team: int = ISHMEM_TEAM_WORLD) -> int:
     return _L.ishmemi_c_fcollect_on_stream(team, dest, source, nbytes, ret or None, stream or None)

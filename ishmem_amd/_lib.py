@@ -45,6 +45,7 @@ PROTOTYPES = [
     ("ishmemi_c_produce_u32", _i, [_vp, _vp, _vp, _sz, _vp]),
     ("ishmemi_c_fcollect", _i, [_i, _vp, _vp, _sz]),
     ("ishmemi_c_fcollect_on_stream", _i, [_i, _vp, _vp, _sz, _vp, _vp]),
+    ("ishmemi_c_collect_on_stream", _i, [_i, _vp, _vp, _sz, _vp, _vp]),
     ("ishmemi_c_collect", _i, [_i, _vp, _vp, _sz]),
     ("ishmemi_c_scan", _i, [_i, _i, _i, _vp, _vp, _sz]),
     ("ishmemi_c_scan_on_stream", _i, [_i, _i, _i, _vp, _vp, _sz, _vp, _vp]),

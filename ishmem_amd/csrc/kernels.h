@@ -116,8 +116,15 @@ struct CollectArgs {
     uint32_t *ep_ctr;  // team's launch words (kEpTeamWords, see kEp*)
     int p, me;
     int unit;  // bytes per item: 16, 4 or 1 (largest dividing every address and length)
+    // Stream-ordered collect (counts not known on the host): this member publishes my_count into
+    // its symmetric count slot before announcing the launch; every workgroup then reads every
+    // member's slot (count_at[j], mapped here) and derives the offsets in team order.
+    uint64_t my_count;
+    uint64_t *my_count_slot;
+    const uint64_t *count_at[kMaxPes];
 };
 hipError_t launch_collect(const CollectArgs &a, int grid, hipStream_t s);
+hipError_t launch_collect_dyn(const CollectArgs &a, int grid, hipStream_t s);
 
 // Inclusive / exclusive prefix sum across the team (MPI_Scan / MPI_Exscan semantics).
 struct ScanArgs {

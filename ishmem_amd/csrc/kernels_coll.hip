@@ -57,6 +57,76 @@ __global__ __launch_bounds__(kBlock) void collect_kernel(CollectArgs a)
     launch_finish(a, ep);
 }
 
+// Member j's `nbytes` at `src` -> dst (local), U-byte items, tiles b, b + G, ... of workgroup b.
+template <int U>
+__device__ __forceinline__ void collect_member(const char *src, char *dst, uint64_t nbytes, bool local,
+                                               uint32_t b, uint64_t G)
+{
+    using Item = std::conditional_t<U == 16, Vec<uint32_t>, std::conditional_t<U == 4, uint32_t, uint8_t>>;
+    const int tid = threadIdx.x;
+    const uint64_t nitems = nbytes / U;
+    for (uint64_t t0 = (uint64_t) b * kTile; t0 < nitems; t0 += G * kTile) {
+        Item x[kUnroll];
+        const char *base = uniform_ptr(src + t0 * U);
+        if (local) {
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint64_t e = (uint64_t) u * kBlock + tid;
+                if (t0 + e < nitems) x[u] = ((const Item *) base)[e];
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint64_t e = (uint64_t) u * kBlock + tid;
+                if (t0 + e < nitems) x[u] = cload<Item>(r, (uint32_t) (e * U));
+            }
+        }
+        Item *dp = (Item *) (dst + t0 * U);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint64_t e = (uint64_t) u * kBlock + tid;
+            if (t0 + e < nitems) dp[e] = x[u];
+        }
+    }
+}
+
+// Stream-ordered collect (ishmemx_<TN>_collect_on_queue, src/ishmemx.h): the counts are not
+// known when the launch is enqueued.  Every workgroup first stores this member's count into its
+// symmetric slot (system-scope, drained) — any workgroup may be the one that announces the
+// launch — so a peer that has seen the announcement reads a final count.  After the start
+// handshake each workgroup reads the p counts (one lane each), derives the team-order offsets
+// and copies every member's bytes with the widest unit that divides that member's source
+// address, destination offset and length.  The slot is not reused before every peer has
+// finished reading it: the next launch starts after this one's "done reading" exchange.
+__global__ __launch_bounds__(kBlock) void collect_dyn_kernel(CollectArgs a)
+{
+    __shared__ uint64_t s_cnt[kMaxPes];
+    const uint32_t b = blockIdx.x;
+    const uint64_t G = gridDim.x;
+    const uint32_t ep = kernel_epoch(a);
+    if (threadIdx.x == 0)
+        __hip_atomic_store(a.my_count_slot, a.my_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    drain_block();
+    const bool ok = launch_start(a, ep);
+    if (ok) {
+        if (threadIdx.x < (unsigned) a.p)
+            s_cnt[threadIdx.x] = __hip_atomic_load(a.count_at[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
+        for (int k = 0; k < a.p; ++k) {
+            const int j = (a.me + ((int) b + k)) % a.p;
+            uint64_t off = 0;
+            for (int i = 0; i < j; ++i) off += s_cnt[i];
+            const uint64_t n = s_cnt[j];
+            const uint64_t al = (uint64_t) a.src[j] | ((uint64_t) a.dst + off) | n;
+            if ((al & 15) == 0) collect_member<16>(a.src[j], a.dst + off, n, j == a.me, b, G);
+            else if ((al & 3) == 0) collect_member<4>(a.src[j], a.dst + off, n, j == a.me, b, G);
+            else collect_member<1>(a.src[j], a.dst + off, n, j == a.me, b, G);
+        }
+    }
+    launch_finish(a, ep);
+}
+
 // Prefix sum.  Phase 1: member c owns chunk c; for each element it folds the members' values in
 // team order and stores every member k's prefix into its own scratch row k (write-through).
 // Phase 2 (once every member has published its chunk): each member pulls its row of every
@@ -259,6 +329,11 @@ hipError_t launch_collect(const CollectArgs &a, int grid, hipStream_t s)
     if (a.unit == 16) return launch_res(collect_kernel<16>, a, grid, s);
     if (a.unit == 4) return launch_res(collect_kernel<4>, a, grid, s);
     return launch_res(collect_kernel<1>, a, grid, s);
+}
+
+hipError_t launch_collect_dyn(const CollectArgs &a, int grid, hipStream_t s)
+{
+    return launch_res(collect_dyn_kernel, a, grid, s);
 }
 
 hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s)

@@ -120,6 +120,7 @@ struct State {
     uint32_t *kern_ep = nullptr;  // [team][kEpTeamWords] launch words of the host-launched kernels
 
     char *team_scratch = nullptr;  // small symmetric buffer for team-management collectives
+    char *count_slots = nullptr;   // symmetric, one 64-B line per team: collect_on_stream counts
     char *staging = nullptr;  // symmetric staging region for non-heap / host buffers
     size_t staging_bytes = 0;
     hipStream_t copy_in = nullptr, copy_out = nullptr;  // staging pipeline streams
@@ -593,6 +594,48 @@ int collect_launch(State &s, int team, void *dst, const void *src, const uint64_
     return 0;
 }
 
+// Stream-ordered collect: the members' counts meet on the device (collect_dyn_kernel), so nothing
+// here waits for the host to learn them.  Count slots: one 64-B line per team (s.count_slots).
+int collect_on_stream_impl(int team, void *dst, const void *src, size_t nbytes, int *ret, hipStream_t st)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.initialized) return fail("collect: not initialized");
+    if (team < 0 || team >= kMaxTeams || !s.teams[team].valid || s.teams[team].my_idx < 0)
+        return fail("collect: invalid team or caller not a member");
+    Team &t = s.teams[team];
+    if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
+    if (t.size == 1) {
+        if (nbytes && dst != src && launch_copy(dst, src, nbytes, st)) return 1;
+        return mark_stream(s, st);
+    }
+    if (!in_heap(s, dst)) return fail("collect: dest must be symmetric-heap memory");
+    if (nbytes && !in_heap(s, src)) return fail("collect: source must be symmetric-heap memory");
+    if (order_stream(s, st)) return 1;
+    CollectArgs a;
+    memset(&a, 0, sizeof(a));
+    std::string why;
+    if (fill_team_sync_args(s, team, a, why)) return fail("collect: " + why);
+    char *slot = s.count_slots + (size_t) team * 64;
+    for (int j = 0; j < t.size; ++j) {
+        const int gpe = t.start + j * t.stride;
+        a.src[j] = nbytes ? translate(s, src, gpe) : s.count_slots;  // an empty source is never read
+        a.count_at[j] = (const uint64_t *) translate(s, slot, gpe);
+        if (!a.src[j] || !a.count_at[j]) return fail("collect: buffer not mapped for PE " + std::to_string(gpe));
+    }
+    a.dst = (char *) dst;
+    a.ret = ret;
+    a.my_count = nbytes;
+    a.my_count_slot = (uint64_t *) slot;
+    // Grid from this member's share (the others' are not known here): the kernel strides over
+    // whatever every member contributes.
+    const uint64_t tile = (uint64_t) kBlock * kUnroll * 16;
+    const uint64_t g = ((uint64_t) t.size * nbytes + tile - 1) / tile;
+    const int grid = (int) std::max<uint64_t>(8, std::min<uint64_t>(g, (uint64_t) s.max_blocks));
+    HIP_TRY(launch_collect_dyn(a, grid, st));
+    return mark_stream(s, st);
+}
+
 int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret, hipStream_t st,
                   bool blocking)
 {
@@ -1001,6 +1044,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     if (!s.staging) return 1;
     s.team_scratch = (char *) heap_alloc(s, kHeapAlign, kHeapAlign);
     if (!s.team_scratch) return 1;
+    s.count_slots = (char *) heap_alloc(s, (size_t) kMaxTeams * 64, kHeapAlign);
+    if (!s.count_slots) return 1;
     HIP_TRY(hipMalloc((void **) &s.dctx, sizeof(ishmemi_c_device_ctx_t)));
     // Launch words: local to this device, touched only by device-scope atomics (work grabs,
     // counters) and system-scope loads/stores (the epoch), which do not depend on the memory
@@ -1507,6 +1552,12 @@ int ishmemi_c_collect(int team, void *dest, const void *source, size_t nbytes)
     if (collect_launch(s, team, dest, source, counts, nullptr, 0) || mark_stream(s, 0)) return 1;
     HIP_TRY(hipStreamSynchronize(0));
     return check_team_errors(s, team);
+}
+
+int ishmemi_c_collect_on_stream(int team, void *dest, const void *source, size_t nbytes, int *ret,
+                                void *stream)
+{
+    return collect_on_stream_impl(team, dest, source, nbytes, ret, (hipStream_t) stream);
 }
 
 int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *source, size_t nelems)

@@ -804,6 +804,37 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                             fails.append(f"pe{pe} collect {tn} counts{counts_c} so{so} do{do} wrong")
                         ish.ishmem_free(dst_b)
                         ish.ishmem_free(src_b)
+            # collect on a stream (ishmemx_<TN>_collect_on_queue): the counts meet on the device.
+            # Three calls chained on one stream with no host synchronisation, counts redrawn per
+            # call (a count slot reused before a peer read it would show), one member empty,
+            # byte / 4-B / 16-B units by alignment; then every dest is compared.
+            st_c = hip.stream_create()
+            ret_c = ish.ishmem_malloc(4)
+            calls = []
+            for c_i, (es_c, so, do) in enumerate(((4, 0, 0), (1, 3, 5), (16, 0, 16))):
+                cnts = [int(x) for x in rng.integers(0, 3000, npes)]
+                cnts[c_i % npes] = 0 if c_i == 1 else cnts[c_i % npes]
+                src_c = ish.ishmem_malloc(3000 * es_c + 64)
+                dst_c = ish.ishmem_malloc(sum(cnts) * es_c + 64)
+                if cnts[pe]:
+                    hip.upload(src_c + so, oracle.collect_pattern_source(pe, cnts[pe], es_c))
+                calls.append((cnts, es_c, so, do, src_c, dst_c))
+            hip.memset(ret_c, 0x7F, 4)
+            ish.ishmem_barrier_all()
+            for cnts, es_c, so, do, src_c, dst_c in calls:
+                if ish.collect_on_stream(dst_c + do, src_c + so, cnts[pe] * es_c, ret_c, st_c) != 0:
+                    fails.append(f"pe{pe} collect_on_stream enqueue {ish.last_error()}")
+            hip.stream_synchronize(st_c)
+            if int(hip.download(ret_c, 1, np.int32)[0]) != 0:
+                fails.append(f"pe{pe} collect_on_stream *ret != 0")
+            for cnts, es_c, so, do, src_c, dst_c in calls:
+                want = oracle.collect_check(cnts, es_c)
+                if want.size and not _bits_equal(hip.download(dst_c + do, want.size, np.uint8), want):
+                    fails.append(f"pe{pe} collect_on_stream es{es_c} counts{cnts} wrong")
+                ish.ishmem_free(dst_c)
+                ish.ishmem_free(src_c)
+            hip.stream_destroy(st_c)
+            ish.ishmem_free(ret_c)
             # fcollectmem of odd byte counts; nelems 0 (still a team sync)
             src_b, dst_b = ish.ishmem_malloc(4096), ish.ishmem_malloc(4096 * npes)
             hip.upload(src_b, oracle.collect_pattern_source(pe, 1001, 1))
