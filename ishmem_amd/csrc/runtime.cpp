@@ -610,7 +610,9 @@ int collect_on_stream_impl(int team, void *dst, const void *src, size_t nbytes, 
         return mark_stream(s, st);
     }
     if (!in_heap(s, dst)) return fail("collect: dest must be symmetric-heap memory");
-    if (nbytes && !in_heap(s, src)) return fail("collect: source must be symmetric-heap memory");
+    // Peers' sources are found at the offset of this PE's (symmetric) source, so it must be in
+    // the heap even when this PE contributes nothing.
+    if (!in_heap(s, src)) return fail("collect: source must be symmetric-heap memory");
     if (order_stream(s, st)) return 1;
     CollectArgs a;
     memset(&a, 0, sizeof(a));
@@ -619,7 +621,7 @@ int collect_on_stream_impl(int team, void *dst, const void *src, size_t nbytes, 
     char *slot = s.count_slots + (size_t) team * 64;
     for (int j = 0; j < t.size; ++j) {
         const int gpe = t.start + j * t.stride;
-        a.src[j] = nbytes ? translate(s, src, gpe) : s.count_slots;  // an empty source is never read
+        a.src[j] = translate(s, src, gpe);
         a.count_at[j] = (const uint64_t *) translate(s, slot, gpe);
         if (!a.src[j] || !a.count_at[j]) return fail("collect: buffer not mapped for PE " + std::to_string(gpe));
     }
