@@ -201,6 +201,7 @@ typedef struct {
     uint32_t *err;                                /* device-API error word (host-visible) */
     int32_t team_start[ISHMEMI_C_MAX_TEAMS], team_stride[ISHMEMI_C_MAX_TEAMS];
     int32_t team_size[ISHMEMI_C_MAX_TEAMS], team_my_idx[ISHMEMI_C_MAX_TEAMS];
+    uint64_t *dev_counts;                         /* symmetric [team][8] u64: device collect counts */
 } ishmemi_c_device_ctx_t;
 void *ishmemi_c_device_ctx(void);
 

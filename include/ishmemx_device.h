@@ -297,6 +297,142 @@ __device__ int reduce_work_group(const ishmemi_c_device_ctx_t *c, int team, T *d
     return reduce_group<work_group_t, T, OP>(c, team, dest, source, nreduce);
 }
 
+// ---- fcollect / collect / sum-scan from inside a kernel ------------------------------------
+// The reference's ishmemx_<TN>_{fcollect,collect,sum_inscan,sum_exscan}_work_group and their
+// device-side blocking forms (src/ishmemx.h, src/collectives/collect_impl.h, scan_impl.h), on the
+// reduce's machinery: start barrier (every member's source final, this group's writes released),
+// pulls with system-coherent loads into the local dest, end barrier (no member returns while a
+// peer may still read its source).
+
+// `nbytes` from `src` (a peer's when `remote`) to the local `dst` by the group: 16-B items when
+// both addresses and the length allow, 4-B or single bytes otherwise.
+template <typename G>
+__device__ inline void group_copy(const char *src, char *dst, size_t nbytes, bool remote)
+{
+    const int tid = G::rank(), nthr = G::size();
+    const uintptr_t al = (uintptr_t) src | (uintptr_t) dst | (uintptr_t) nbytes;
+    if ((al & 15) == 0) {
+        const size_t nv = nbytes / 16;
+        for (size_t v0 = 0; v0 < nv; v0 += (size_t) nthr * kUnroll) {
+            const char *step = group_uniform(src + v0 * 16);
+            Vec16<uint32_t> x[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const size_t k = (size_t) u * nthr + tid;
+                if (v0 + k < nv)
+                    x[u] = remote ? sys_load16<uint32_t>(step, (uint32_t) (k * 16)) : ((const Vec16<uint32_t> *) step)[k];
+            }
+            Vec16<uint32_t> *dp = (Vec16<uint32_t> *) (dst + v0 * 16);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const size_t k = (size_t) u * nthr + tid;
+                if (v0 + k < nv) dp[k] = x[u];
+            }
+        }
+    } else if ((al & 3) == 0) {
+        for (size_t i = tid; i < nbytes / 4; i += nthr)
+            ((uint32_t *) dst)[i] = remote ? sys_load((const uint32_t *) src + i) : ((const uint32_t *) src)[i];
+    } else {
+        for (size_t i = tid; i < nbytes; i += nthr)
+            dst[i] = remote ? (char) sys_load((const uint8_t *) src + i) : src[i];
+    }
+}
+
+template <typename G>
+__device__ inline uint32_t group_epoch(const ishmemi_c_device_ctx_t *c, int team)
+{
+    uint32_t epoch = 0;
+    if (G::rank() == 0)
+        epoch = __hip_atomic_fetch_add(c->epochs + team, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    return G::bcast(epoch);
+}
+
+// fcollect (equal counts) when counts == nullptr; collect otherwise: this member contributes
+// `mybytes`, published in its symmetric count slot before the start barrier and read by every
+// member after it (pull: no peer stores into this PE's coarse-grained heap).
+template <typename G>
+__device__ inline int collect_group(const ishmemi_c_device_ctx_t *c, int team, void *dest, const void *source,
+                                    size_t mybytes, bool equal)
+{
+    const int size = c->team_size[team], me = c->team_my_idx[team];
+    if (size <= 0 || me < 0) return 1;
+    const uint32_t epoch = group_epoch<G>(c, team);
+    if (size == 1) {
+        if (dest != source) group_copy<G>((const char *) source, (char *) dest, mybytes, false);
+        G::sync();
+        return 0;
+    }
+    uint64_t *slot = c->dev_counts + (size_t) team * 8;
+    if (!equal && G::rank() == 0) sys_store(slot, (uint64_t) mybytes);  // write-through; barrier drains it
+    if (!group_barrier<G>(c, team, 0, epoch, true)) return 1;
+    const int start = c->team_start[team], stride = c->team_stride[team];
+    size_t off = 0;
+    for (int j = 0; j < size; ++j) {
+        const int gpe = start + j * stride;
+        const size_t nb = equal ? mybytes : (size_t) sys_load((const uint64_t *) peer_addr(c, slot, gpe));
+        if (nb) {
+            const char *src = j == me ? (const char *) source : peer_addr(c, source, gpe);
+            group_copy<G>(src, (char *) dest + off, nb, j != me);
+        }
+        off += nb;
+    }
+    return group_barrier<G>(c, team, 2, epoch, false) ? 0 : 1;
+}
+
+// Prefix sum in team order: member me folds members 0..me (inclusive) or 0..me-1 (exclusive;
+// member 0 gets 0) element by element — the first term passes through unchanged, as in the host
+// scan.  dest must not overlap source (a peer may still be reading it).
+template <typename G, typename T>
+__device__ inline int scan_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, const T *source,
+                                 size_t nelems, bool inclusive)
+{
+    const int tid = G::rank(), nthr = G::size();
+    const int size = c->team_size[team], me = c->team_my_idx[team];
+    if (size <= 0 || me < 0) return 1;
+    const uint32_t epoch = group_epoch<G>(c, team);
+    if (size > 1 && dest == source) return 1;
+    if (size > 1 && !group_barrier<G>(c, team, 0, epoch, true)) return 1;
+    const int last = inclusive ? me : me - 1;
+    const int start = c->team_start[team], stride = c->team_stride[team];
+    constexpr size_t E = 16 / sizeof(T);
+    const bool vec = ((((uintptr_t) dest) | ((uintptr_t) source)) & 15) == 0;
+    const size_t nv = vec ? nelems / E : 0;
+    for (size_t v0 = 0; v0 < nv; v0 += (size_t) nthr * kUnroll) {
+        Vec16<T> acc[kUnroll] = {};
+        for (int k = 0; k <= last; ++k) {
+            const char *base = k == me ? (const char *) source : peer_addr(c, source, start + k * stride);
+            const char *step = group_uniform(base + v0 * 16);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const size_t q = (size_t) u * nthr + tid;
+                if (v0 + q < nv) {
+                    const Vec16<T> x = sys_load16<T>(step, (uint32_t) (q * 16));
+                    acc[u] = k == 0 ? x : op16<T, ISHMEMI_OP_SUM>(acc[u], x);
+                }
+            }
+        }
+        Vec16<T> *dp = (Vec16<T> *) dest + v0;
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const size_t q = (size_t) u * nthr + tid;
+            if (v0 + q < nv) dp[q] = acc[u];
+        }
+    }
+    for (size_t i = nv * E + tid; i < nelems; i += nthr) {
+        T acc = T();
+        for (int k = 0; k <= last; ++k) {
+            const T x = k == me ? source[i] : sys_load((const T *) peer_addr(c, source + i, start + k * stride));
+            acc = k == 0 ? x : op1<T, ISHMEMI_OP_SUM>(acc, x);
+        }
+        dest[i] = acc;
+    }
+    if (size == 1) {
+        G::sync();
+        return 0;
+    }
+    return group_barrier<G>(c, team, 2, epoch, false) ? 0 : 1;
+}
+
 template <typename T>
 constexpr bool is_canon()
 {
@@ -373,6 +509,107 @@ ISHMEMX_DEV_GENERIC(prod, ISHMEMI_OP_PROD)
                                                                            source, nreduce);       \
     }
 
+/* fcollect / collect / sum_inscan / sum_exscan: work-group (or wavefront) and one-work-item forms
+ * for the reference's 23 arithmetic typenames, plus fcollectmem / collectmem. */
+#define ISHMEMX_DEV_COLL(TYPENAME, TYPE, UNUSED1, UNUSED2)                                          \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
+    __device__ inline int ishmemx_##TYPENAME##_fcollect_work_group(                                \
+        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source, size_t nelems, \
+        G = G())                                                                                   \
+    {                                                                                              \
+        return ishmemx_dev::collect_group<G>(ctx, team, dest, source, nelems * sizeof(TYPE), true); \
+    }                                                                                              \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
+    __device__ inline int ishmemx_##TYPENAME##_fcollect_work_group(                                \
+        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nelems, G = G())  \
+    {                                                                                              \
+        return ishmemx_##TYPENAME##_fcollect_work_group<G>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source, \
+                                                           nelems);                                \
+    }                                                                                              \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
+    __device__ inline int ishmemx_##TYPENAME##_collect_work_group(                                 \
+        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source, size_t nelems, \
+        G = G())                                                                                   \
+    {                                                                                              \
+        return ishmemx_dev::collect_group<G>(ctx, team, dest, source, nelems * sizeof(TYPE), false); \
+    }                                                                                              \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
+    __device__ inline int ishmemx_##TYPENAME##_collect_work_group(                                 \
+        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nelems, G = G())  \
+    {                                                                                              \
+        return ishmemx_##TYPENAME##_collect_work_group<G>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,  \
+                                                          nelems);                                 \
+    }                                                                                              \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
+    __device__ inline int ishmemx_##TYPENAME##_sum_inscan_work_group(                              \
+        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source, size_t nelems, \
+        G = G())                                                                                   \
+    {                                                                                              \
+        return ishmemx_dev::scan_group<G, TYPE>(ctx, team, dest, source, nelems, true);            \
+    }                                                                                              \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
+    __device__ inline int ishmemx_##TYPENAME##_sum_inscan_work_group(                              \
+        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nelems, G = G())  \
+    {                                                                                              \
+        return ishmemx_dev::scan_group<G, TYPE>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source, nelems,   \
+                                                true);                                             \
+    }                                                                                              \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
+    __device__ inline int ishmemx_##TYPENAME##_sum_exscan_work_group(                              \
+        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source, size_t nelems, \
+        G = G())                                                                                   \
+    {                                                                                              \
+        return ishmemx_dev::scan_group<G, TYPE>(ctx, team, dest, source, nelems, false);           \
+    }                                                                                              \
+    template <typename G = ishmemx_dev::work_group_t>                                              \
+    __device__ inline int ishmemx_##TYPENAME##_sum_exscan_work_group(                              \
+        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nelems, G = G())  \
+    {                                                                                              \
+        return ishmemx_dev::scan_group<G, TYPE>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source, nelems,   \
+                                                false);                                            \
+    }                                                                                              \
+    __device__ inline int ishmem_##TYPENAME##_fcollect(const ishmemi_c_device_ctx_t *ctx, int team, \
+                                                       TYPE *dest, const TYPE *source,             \
+                                                       size_t nelems)                              \
+    {                                                                                              \
+        return ishmemx_dev::collect_group<ishmemx_dev::thread_t>(ctx, team, dest, source,          \
+                                                                 nelems * sizeof(TYPE), true);     \
+    }                                                                                              \
+    __device__ inline int ishmem_##TYPENAME##_collect(const ishmemi_c_device_ctx_t *ctx, int team, \
+                                                      TYPE *dest, const TYPE *source,              \
+                                                      size_t nelems)                               \
+    {                                                                                              \
+        return ishmemx_dev::collect_group<ishmemx_dev::thread_t>(ctx, team, dest, source,          \
+                                                                 nelems * sizeof(TYPE), false);    \
+    }                                                                                              \
+    __device__ inline int ishmem_##TYPENAME##_sum_inscan(const ishmemi_c_device_ctx_t *ctx,        \
+                                                         int team, TYPE *dest, const TYPE *source, \
+                                                         size_t nelems)                            \
+    {                                                                                              \
+        return ishmemx_dev::scan_group<ishmemx_dev::thread_t, TYPE>(ctx, team, dest, source,       \
+                                                                    nelems, true);                 \
+    }                                                                                              \
+    __device__ inline int ishmem_##TYPENAME##_sum_exscan(const ishmemi_c_device_ctx_t *ctx,        \
+                                                         int team, TYPE *dest, const TYPE *source, \
+                                                         size_t nelems)                            \
+    {                                                                                              \
+        return ishmemx_dev::scan_group<ishmemx_dev::thread_t, TYPE>(ctx, team, dest, source,       \
+                                                                    nelems, false);                \
+    }
+
+template <typename G = ishmemx_dev::work_group_t>
+__device__ inline int ishmemx_fcollectmem_work_group(const ishmemi_c_device_ctx_t *ctx, int team, void *dest,
+                                                     const void *source, size_t nbytes, G = G())
+{
+    return ishmemx_dev::collect_group<G>(ctx, team, dest, source, nbytes, true);
+}
+template <typename G = ishmemx_dev::work_group_t>
+__device__ inline int ishmemx_collectmem_work_group(const ishmemi_c_device_ctx_t *ctx, int team, void *dest,
+                                                    const void *source, size_t nbytes, G = G())
+{
+    return ishmemx_dev::collect_group<G>(ctx, team, dest, source, nbytes, false);
+}
+
 /* Same TYPENAME x op matrix as the host API (src/collectives/reduce.cpp:95-417). */
 #define ISHMEMX_DEV_BITWISE_TYPES(X, OPNAME, OPC)                                                   \
     X(uchar, unsigned char, OPNAME, OPC) X(ushort, unsigned short, OPNAME, OPC)                    \
@@ -399,5 +636,6 @@ ISHMEMX_DEV_ARITH_TYPES(ISHMEMX_DEV_TYPED, max, ISHMEMI_OP_MAX)
 ISHMEMX_DEV_ARITH_TYPES(ISHMEMX_DEV_TYPED, min, ISHMEMI_OP_MIN)
 ISHMEMX_DEV_ARITH_TYPES(ISHMEMX_DEV_TYPED, sum, ISHMEMI_OP_SUM)
 ISHMEMX_DEV_ARITH_TYPES(ISHMEMX_DEV_TYPED, prod, ISHMEMI_OP_PROD)
+ISHMEMX_DEV_ARITH_TYPES(ISHMEMX_DEV_COLL, _, _)
 
 #endif /* ISHMEM_AMD_ISHMEMX_DEVICE_H */

@@ -803,6 +803,7 @@ int sync_device_ctx(State &s)
     }
     c.my_dflags = dev_flags(s.flags);
     c.epochs = s.dev_epochs;
+    c.dev_counts = (uint64_t *) (s.count_slots + (size_t) kMaxTeams * 64);
     c.err = s.err_dev + kMaxTeams;
     for (int t = 0; t < kMaxTeams; ++t) {
         const Team &tm = s.teams[t];
@@ -1046,7 +1047,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     if (!s.staging) return 1;
     s.team_scratch = (char *) heap_alloc(s, kHeapAlign, kHeapAlign);
     if (!s.team_scratch) return 1;
-    s.count_slots = (char *) heap_alloc(s, (size_t) kMaxTeams * 64, kHeapAlign);
+    // [0, kMaxTeams) lines: collect_on_stream; [kMaxTeams, 2 kMaxTeams): the device API's collect.
+    s.count_slots = (char *) heap_alloc(s, (size_t) 2 * kMaxTeams * 64, kHeapAlign);
     if (!s.count_slots) return 1;
     HIP_TRY(hipMalloc((void **) &s.dctx, sizeof(ishmemi_c_device_ctx_t)));
     // Launch words: local to this device, touched only by device-scope atomics (work grabs,

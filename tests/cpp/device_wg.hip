@@ -3,7 +3,8 @@
 // work-group per PE, checked against the closed form ((1 << npes) - 1) << 40 + idx * npes) and
 // of its reduce_*.cpp pattern tests (sources = reference source patterns, checked against the
 // reference check patterns restated in oracle/oracle.c, linked here as the CHECKER).
-// Also: a wavefront (sub_group) caller and a single work-item device-side ishmem_int_sum_reduce.
+// Also: a wavefront (sub_group) caller and a single work-item device-side ishmem_int_sum_reduce,
+// and the device-side fcollect / collect / sum_inscan / sum_exscan (closed-form checks).
 // Launch: ISHMEM_PE=<pe> ISHMEM_NPES=<n> ISHMEM_DEVICE=0 ISHMEM_BOOTSTRAP_KEY=<k> ./device_wg
 #include <hip/hip_runtime.h>
 
@@ -84,6 +85,73 @@ __global__ void single_kernel(const ishmemi_c_device_ctx_t *ctx, int *dest, cons
                               int *rc)
 {
     *rc = ishmem_int_sum_reduce(ctx, ISHMEM_TEAM_WORLD, dest, source, n);
+}
+
+// Device-side fcollect / collect / sum-scan (src/ishmemx.h *_work_group): the source is produced
+// in the same kernel, then the collective runs by the work-group (or one wavefront / one item).
+template <int MODE>  // 0 fcollect, 1 collect, 2 inscan, 3 exscan, 4 fcollect by a wavefront,
+                     // 5 inscan by one work-item
+__global__ void coll_kernel(const ishmemi_c_device_ctx_t *ctx, long *dest, long *source, size_t n, int my_pe,
+                            int *rc)
+{
+    const size_t mine = MODE == 1 ? n + 37 * (size_t) my_pe : n;  // collect: counts differ per PE
+    for (size_t i = threadIdx.x; i < mine; i += blockDim.x) source[i] = ((long) (my_pe + 1) << 32) + (long) i;
+    int r = 0;
+    if constexpr (MODE == 0) r = ishmemx_long_fcollect_work_group(ctx, dest, (const long *) source, n);
+    else if constexpr (MODE == 1) r = ishmemx_long_collect_work_group(ctx, dest, (const long *) source, mine);
+    else if constexpr (MODE == 2) r = ishmemx_long_sum_inscan_work_group(ctx, dest, (const long *) source, n);
+    else if constexpr (MODE == 3) r = ishmemx_long_sum_exscan_work_group(ctx, dest, (const long *) source, n);
+    else if constexpr (MODE == 4) {
+        __syncthreads();  // every wave's source stores are done before one wavefront publishes them
+        if (threadIdx.x / warpSize != 0) return;
+        r = ishmemx_long_fcollect_work_group(ctx, dest, (const long *) source, n, ishmemx_dev::wavefront);
+        if (__lane_id() == 0) *rc = r;
+        return;
+    } else {
+        __syncthreads();
+        if (threadIdx.x != 0) return;
+        r = ishmem_long_sum_inscan(ctx, ISHMEM_TEAM_WORLD, dest, (const long *) source, n);
+        *rc = r;
+        return;
+    }
+    if (threadIdx.x == 0) *rc = r;
+}
+
+template <int MODE>
+static void coll_case(const ishmemi_c_device_ctx_t *ctx, size_t n, int block, char *sb, char *db, int *rc)
+{
+    const int pe = ishmem_my_pe(), npes = ishmem_n_pes();
+    auto val = [](int j, size_t i) { return ((long) (j + 1) << 32) + (long) i; };
+    std::vector<long> want;
+    if (MODE == 0 || MODE == 1 || MODE == 4) {
+        for (int j = 0; j < npes; ++j) {
+            const size_t c = MODE == 1 ? n + 37 * (size_t) j : n;
+            for (size_t i = 0; i < c; ++i) want.push_back(val(j, i));
+        }
+    } else {
+        const int last = (MODE == 3) ? pe - 1 : pe;
+        for (size_t i = 0; i < n; ++i) {
+            long acc = 0;
+            for (int k = 0; k <= last; ++k) acc += val(k, i);
+            want.push_back(acc);
+        }
+    }
+    (void) hipMemset(db, 0xA5, want.size() * sizeof(long) + 64);
+    (void) hipMemset(rc, 0xff, sizeof(int));
+    hipLaunchKernelGGL(coll_kernel<MODE>, dim3(1), dim3(block), 0, 0, ctx, (long *) db, (long *) sb, n, pe, rc);
+    (void) hipDeviceSynchronize();
+    int r = -1;
+    std::vector<long> got(want.size() + 8);
+    (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);
+    (void) hipMemcpy(got.data(), db, got.size() * sizeof(long), hipMemcpyDeviceToHost);
+    size_t bad = 0;
+    for (size_t i = 0; i < want.size(); ++i) bad += got[i] != want[i];
+    const long guard = (long) 0xA5A5A5A5A5A5A5A5ull;
+    for (size_t i = want.size(); i < got.size(); ++i) bad += got[i] != guard;
+    if (r != 0 || bad) {
+        if (++errors <= 16) printf("[%d] FAIL device collective mode %d n %zu block %d rc %d bad %zu\n", pe, MODE, n,
+                                   block, r, bad);
+    }
 }
 
 template <typename K, typename T, int OPC, int ODT>
@@ -215,6 +283,16 @@ int main()
                                                                     n, sb, db, rc);
         group_case<decltype(&single_kernel), int, OR_SUM, OD_INT32>("single-thread int sum", single_kernel, 1,
                                                                     ctx, n, sb, db, rc);
+    }
+    // fcollect / collect / inscan / exscan from inside a kernel (dest room: npes * (n + 37 npes)).
+    for (size_t n : {1, 5, 64, 1000, 4099}) {
+        if ((size_t) npes * (n + 37 * (size_t) npes) + 16 > maxn) continue;
+        coll_case<0>(ctx, n, 256, sb, db, rc);
+        coll_case<1>(ctx, n, 256, sb, db, rc);
+        coll_case<2>(ctx, n, 256, sb, db, rc);
+        coll_case<3>(ctx, n, 1024, sb, db, rc);
+        coll_case<4>(ctx, n, 128, sb, db, rc);
+        coll_case<5>(ctx, n, 64, sb, db, rc);
     }
     ishmem_free(rc);
     ishmem_free(db);
