@@ -388,9 +388,8 @@ __device__ inline int scan_group(const ishmemi_c_device_ctx_t *c, int team, T *d
 {
     const int tid = G::rank(), nthr = G::size();
     const int size = c->team_size[team], me = c->team_my_idx[team];
-    if (size <= 0 || me < 0) return 1;
+    if (size <= 0 || me < 0 || (size > 1 && dest == source)) return 1;
     const uint32_t epoch = group_epoch<G>(c, team);
-    if (size > 1 && dest == source) return 1;
     if (size > 1 && !group_barrier<G>(c, team, 0, epoch, true)) return 1;
     const int last = inclusive ? me : me - 1;
     const int start = c->team_start[team], stride = c->team_stride[team];
