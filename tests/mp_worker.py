@@ -570,6 +570,47 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             ish.ishmem_free(d_base)
             ish.ishmem_free(s_base)
 
+        if "huge8" in scenarios:
+            # More than 2^32 ELEMENTS per PE (4.5 GiB of uint8, xor) from a misaligned start: any
+            # 32-bit element index or byte offset in the path would alias chunk k + 256 onto chunk
+            # k.  Source: a 16 MiB base block per PE; PE 0's is xor-tagged per 16 MiB chunk so
+            # that chunks k and k + 256 of the result differ.
+            blk = 16 << 20
+            n = (9 << 29) + 5  # 4.5 GiB + 5 B
+            s_base = ish.ishmem_malloc(n + 64)
+            d_base = ish.ishmem_malloc(n + 64)
+            if not (s_base and d_base):
+                raise RuntimeError(f"huge8 heap: {ish.last_error()}")
+            s, d = s_base + 3, d_base + 3
+
+            def base_of(j):
+                i = np.arange(blk, dtype=np.uint32)
+                return ((i * 2654435761 + j * 40503) >> 13).astype(np.uint8)
+
+            def tag(k):
+                return np.uint8((k * 7 + (k >> 8) * 13 + 1) & 0xFF)
+
+            mine = base_of(pe)
+            for k in range((n + blk - 1) // blk):
+                m = min(blk, n - k * blk)
+                hip.upload(s + k * blk, mine[:m] ^ tag(k) if pe == 0 else mine[:m])  # tag on PE 0 only
+            r = ish.reduce("xor", "uint8", d, s, n)
+            if r:
+                fails.append(f"pe{pe} huge8 rc={r} {ish.last_error()}")
+            else:
+                allb = np.bitwise_xor.reduce([base_of(j) for j in range(npes)])
+                for lo in (0, (1 << 32) - 2048, (1 << 32) + 12345, n - 4096, (256 << 24) + 77):
+                    m = min(4096, n - lo)
+                    got = hip.download(d + lo, m, np.uint8)
+                    idx = np.arange(lo, lo + m)
+                    want = allb[idx % blk] ^ np.array([tag(int(k)) for k in idx // blk], np.uint8)
+                    if not np.array_equal(got, want):
+                        fails.append(f"pe{pe} huge8: wrong bytes near {lo} ({int(np.sum(got != want))})")
+                    elif pe == 0:
+                        print(f"[huge8] pe0 {m} bytes at {lo} match ({n} B per PE)", flush=True)
+            ish.ishmem_free(d_base)
+            ish.ishmem_free(s_base)
+
         if "occupied" in scenarios:
             # Residency independence: PE 0 first enqueues, on another stream, a kernel holding all
             # but 16 CUs (two 1024-work-item, 80 KiB-LDS workgroups per CU) for 4 s; then the PEs

@@ -179,3 +179,9 @@ def test_flag_memory_kinds_agree_and_work(kinds):
     # and the collectives (LL, RS + AG, fcollect, scan) work on each kind.
     run_pes(len(kinds), ["flagkind", "inplace", "edge", "stream"],
             env={"ISHMEM_FLAGS_KIND": kinds, "FLAGKIND_WANT": max(kinds)})
+
+
+def test_more_than_2pow32_elements_uint8_xor():
+    # 4.5 GiB of uint8 per PE (> 2^32 elements) from a misaligned start, xor over 2 PEs: windows
+    # around the 2^32 element / byte boundary, a chunk aliasing point and the ragged end.
+    run_pes(2, ["huge8"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "10G"}, timeout=500)
