@@ -570,6 +570,53 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             ish.ishmem_free(d_base)
             ish.ishmem_free(s_base)
 
+        if "concurrent" in scenarios and npes >= 4 and npes % 2 == 0:
+            # Collectives of different teams in flight at once on different streams (the TP / DP
+            # groups of a 2-D split): an x-team and a y-team reduce, each 16 Mi floats, enqueued
+            # back to back on two streams with no synchronisation, plus a WORLD LL reduce on a
+            # third; every team has its own flag block and launch words, and no kernel needs its
+            # grid resident, so they overlap in any interleaving.  Three rounds, inputs redrawn.
+            r, xt, yt = ish.ishmem_team_split_2d(ish.ISHMEM_TEAM_WORLD, 2)
+            if r:
+                fails.append(f"pe{pe} concurrent split: {ish.last_error()}")
+            else:
+                xm = [j for j in range(npes) if j // 2 == pe // 2]
+                ym = [j for j in range(npes) if j % 2 == pe % 2]
+                n, nsmall = 16 << 20, 3000
+                sx, dx, sy, dy = (heap(n, DT["float"]) for _ in range(4))
+                sw, dw = heap(nsmall, DT["int32"]), heap(nsmall, DT["int32"])
+                ret = ish.ishmem_malloc(12)
+                sts = [hip.stream_create() for _ in range(3)]
+                for rnd in range(3):
+                    ax = {j: oracle.fill_random(DT["float"], 0xC0 + 16 * rnd + j, n) for j in xm}
+                    ay = {j: oracle.fill_random(DT["float"], 0xD0 + 16 * rnd + j, n) for j in ym}
+                    aw = [oracle.fill_random(DT["int32"], 0xE0 + 16 * rnd + j, nsmall) for j in range(npes)]
+                    hip.upload(sx, ax[pe])
+                    hip.upload(sy, ay[pe])
+                    hip.upload(sw, aw[pe])
+                    hip.memset(ret, 0x7F, 12)
+                    ish.ishmem_barrier_all()
+                    rc = [ish.reduce_on_stream("sum", "float", dx, sx, n, ret, sts[0], xt),
+                          ish.reduce_on_stream("sum", "float", dy, sy, n, ret + 4, sts[1], yt),
+                          ish.reduce_on_stream("max", "int32", dw, sw, nsmall, ret + 8, sts[2])]
+                    for st_ in sts:
+                        hip.stream_synchronize(st_)
+                    rets = hip.download(ret, 3, np.int32)
+                    if any(rc) or np.any(rets != 0):
+                        fails.append(f"pe{pe} concurrent round {rnd}: rc={rc} ret={rets} {ish.last_error()}")
+                        break
+                    check(f"concurrent x {rnd}", OPS["sum"], DT["float"], [ax[j] for j in xm],
+                          hip.download(dx, n, np.float32), me=xm.index(pe))
+                    check(f"concurrent y {rnd}", OPS["sum"], DT["float"], [ay[j] for j in ym],
+                          hip.download(dy, n, np.float32), me=ym.index(pe))
+                    check(f"concurrent world {rnd}", OPS["max"], DT["int32"], aw, hip.download(dw, nsmall, np.int32))
+                for st_ in sts:
+                    hip.stream_destroy(st_)
+                for b_ in (ret, dw, sw, dy, sy, dx, sx):
+                    ish.ishmem_free(b_)
+                ish.ishmem_team_destroy(xt)
+                ish.ishmem_team_destroy(yt)
+
         if "huge8" in scenarios:
             # More than 2^32 ELEMENTS per PE (4.5 GiB of uint8, xor) from a misaligned start: any
             # 32-bit element index or byte offset in the path would alias chunk k + 256 onto chunk

@@ -185,3 +185,10 @@ def test_more_than_2pow32_elements_uint8_xor():
     # 4.5 GiB of uint8 per PE (> 2^32 elements) from a misaligned start, xor over 2 PEs: windows
     # around the 2^32 element / byte boundary, a chunk aliasing point and the ragged end.
     run_pes(2, ["huge8"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "10G"}, timeout=500)
+
+
+@pytest.mark.parametrize("npes", [4, 8])
+def test_concurrent_collectives_of_different_teams_on_different_streams(npes):
+    # x-team and y-team reduces of a 2-D split plus a WORLD reduce in flight together on three
+    # streams (TP / DP groups), no synchronisation between them; full grids per PE.
+    run_pes(npes, ["concurrent"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "1G"}, timeout=300)
