@@ -376,6 +376,28 @@ def rccl_allreduce(dist, device, n, B, world, steps, line, limit_s=240.0):
         wd.cancel()
 
 
+def mpich_baseline(ns: int) -> list | dict:
+    """The same host path with the reference's own runtime call on the host side: MPICH's
+    MPI_Allreduce on each 64 KiB bounce chunk (runtime_mpi.cpp:802-812), p processes under
+    mpiexec, all on this GPU (oracle/mpi_bounce.c; built by __graft_entry__.build when MPICH is
+    installed).  Per-PE GiB/s of the slowest rank, result checked on every rank."""
+    exe, mpiexec = ROOT / "oracle" / "mpi_bounce", Path("/opt/conda/bin/mpiexec")
+    if not (exe.exists() and mpiexec.exists()):
+        return {"error": "MPICH (/opt/conda) or oracle/mpi_bounce not present"}
+    out = []
+    for p in (1, 2, 4, 8):
+        try:
+            r = subprocess.run([str(mpiexec), "-n", str(p), str(exe), str(ns), "1"], cwd=str(ROOT),
+                               capture_output=True, text=True, timeout=120)
+            t, nbytes, bad = r.stdout.split()[-3:]
+            out.append({"pes": p, "value": int(nbytes) / GiB / float(t), "unit": "GiB/s (per PE)",
+                        "cores": p, "checked": r.returncode == 0 and int(bad) == 0,
+                        "sample": f"{int(nbytes) >> 20} MiB f32 per PE, MPICH MPI_Allreduce per 64 KiB chunk"})
+        except Exception as ex:
+            out.append({"pes": p, "error": f"{type(ex).__name__}: {ex}"})
+    return out
+
+
 def cpu_baseline_leg(ish, hip, src, dst, n, B, world, rank, dist, key) -> tuple[dict, dict]:
     """The reference's host path, restated in oracle/ and timed on the host cores
     (reduce_impl.h:186-228 -> memory.cpp:310-321 -> runtime_mpi.cpp:802-812): every 64 KiB chunk
@@ -428,6 +450,7 @@ def cpu_baseline_leg(ish, hip, src, dst, n, B, world, rank, dist, key) -> tuple[
                 if h.poll() is None:
                     h.kill()
     extra["cpu_baseline_pes"] = side
+    extra["cpu_baseline_mpich"] = mpich_baseline(ns)
     tm = oracle.host_proxy_time(op, dt, n, 1, 2)
     extra["cpu_baseline_memcpy_only"] = {
         "value": B / GiB / tm, "unit": "GiB/s", "cores": 1, "kind": "port",
