@@ -376,18 +376,19 @@ def rccl_allreduce(dist, device, n, B, world, steps, line, limit_s=240.0):
         wd.cancel()
 
 
-def mpich_baseline(ns: int) -> list | dict:
+def mpich_baseline(ns: int, pes=(1, 2, 4, 8), device_mod: int = 1) -> list | dict:
     """The same host path with the reference's own runtime call on the host side: MPICH's
     MPI_Allreduce on each 64 KiB bounce chunk (runtime_mpi.cpp:802-812), p processes under
     mpiexec, all on this GPU (oracle/mpi_bounce.c; built by __graft_entry__.build when MPICH is
-    installed).  Per-PE GiB/s of the slowest rank, result checked on every rank."""
+    installed).  Per-PE GiB/s of the slowest rank, result checked on every rank.  device_mod: the
+    MPI ranks use devices rank % device_mod (1: all on this GPU; N>1 runs pass N, one per GPU)."""
     exe, mpiexec = ROOT / "oracle" / "mpi_bounce", Path("/opt/conda/bin/mpiexec")
     if not (exe.exists() and mpiexec.exists()):
         return {"error": "MPICH (/opt/conda) or oracle/mpi_bounce not present"}
     out = []
-    for p in (1, 2, 4, 8):
+    for p in pes:
         try:
-            r = subprocess.run([str(mpiexec), "-n", str(p), str(exe), str(ns), "1"], cwd=str(ROOT),
+            r = subprocess.run([str(mpiexec), "-n", str(p), str(exe), str(ns), str(device_mod)], cwd=str(ROOT),
                                capture_output=True, text=True, timeout=120)
             t, nbytes, bad = r.stdout.split()[-3:]
             out.append({"pes": p, "value": int(nbytes) / GiB / float(t), "unit": "GiB/s (per PE)",
@@ -416,6 +417,11 @@ def cpu_baseline_leg(ish, hip, src, dst, n, B, world, rank, dist, key) -> tuple[
         ns = min(n, (64 << 20) // 4)
         t = oracle.host_bounce_time(op, dt, ns, rank, world, key + "cpu", src, dst, reps=1)
         t = max_over_ranks(dist, [t])[0]
+        # The same with MPICH's MPI_Allreduce, N processes one per GPU (rank 0 launches them while
+        # the bench ranks wait).
+        if rank == 0:
+            extra["cpu_baseline_mpich"] = mpich_baseline(ns, pes=(world,), device_mod=world)
+        dist.barrier()
         return ({"value": ns * 4 / GiB / t, "unit": "GiB/s", "cores": world, "kind": "port",
                  "per": "per PE (B/t, compare algbw_GiBps)",
                  "whole_job_GiBps": world * ns * 4 / GiB / t,
