@@ -566,7 +566,7 @@ int fill_team_sync_args(State &s, int team, A &a, std::string &why)
 
 // nbytes[j] = bytes member j contributes; dest slot of j starts at the sum of the earlier ones.
 int collect_launch(State &s, int team, void *dst, const void *src, const uint64_t *nbytes, int *ret,
-                   hipStream_t st)
+                   hipStream_t st, const uint64_t *dst_off = nullptr)
 {
     Team &t = s.teams[team];
     if (order_stream(s, st)) return 1;
@@ -579,9 +579,9 @@ int collect_launch(State &s, int team, void *dst, const void *src, const uint64_
         const int gpe = t.start + j * t.stride;
         a.src[j] = translate(s, src, gpe);
         if (!a.src[j]) return fail("collect: source must be symmetric-heap memory");
-        a.dst_off[j] = off;
+        a.dst_off[j] = dst_off ? dst_off[j] : off;
         a.nbytes[j] = nbytes[j];
-        orv |= off | nbytes[j];
+        orv |= a.dst_off[j] | nbytes[j];
         off += nbytes[j];
         maxb = std::max(maxb, nbytes[j]);
     }
@@ -592,6 +592,52 @@ int collect_launch(State &s, int team, void *dst, const void *src, const uint64_
     const int grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((items + tile - 1) / tile, s.max_blocks));
     HIP_TRY(launch_collect(a, grid, st));
     return 0;
+}
+
+// Memory a kernel of this device may write: the heap, device memory, pinned host memory.
+bool device_writable(const State &s, const void *p)
+{
+    if (in_heap(s, p)) return true;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void) hipGetLastError();
+        return false;  // pageable host memory
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged ||
+           (attr.type == hipMemoryTypeHost && attr.devicePointer != nullptr);
+}
+
+// fcollect / collect with a source outside the heap (host or plain device memory, which peers
+// cannot map): like the reference's intra-node collect, which copies from any local source
+// (src/collectives/collect_impl.h:93-114), the bytes go through the symmetric staging region,
+// segment by segment — copy this member's part of segment k in, then the pull collect of segment k
+// from every member's staging region.  A member's next copy follows its kernel, which returns only
+// after every peer has finished reading its staging region ("done reading").
+int collect_staged(State &s, int team, char *dst, const char *src, const uint64_t *nbytes, int *ret,
+                   hipStream_t st)
+{
+    const Team &t = s.teams[team];
+    const uint64_t S = (uint64_t) s.staging_bytes & ~(uint64_t) 15;
+    uint64_t maxb = 0, off[kMaxPes], acc = 0;
+    for (int j = 0; j < t.size; ++j) {
+        off[j] = acc;
+        acc += nbytes[j];
+        maxb = std::max<uint64_t>(maxb, nbytes[j]);
+    }
+    const uint64_t nseg = std::max<uint64_t>(1, (maxb + S - 1) / S);
+    if (staging_acquire(s, st)) return 1;
+    for (uint64_t k = 0; k < nseg; ++k) {
+        uint64_t segb[kMaxPes], segoff[kMaxPes];
+        for (int j = 0; j < t.size; ++j) {
+            const uint64_t lo = std::min<uint64_t>(nbytes[j], k * S);
+            segb[j] = std::min<uint64_t>(S, nbytes[j] - lo);
+            segoff[j] = off[j] + lo;
+        }
+        const uint64_t mine = segb[t.my_idx];
+        if (mine) HIP_TRY(hipMemcpyAsync(s.staging, src + k * S, mine, hipMemcpyDefault, st));
+        if (collect_launch(s, team, dst, s.staging, segb, ret, st, segoff)) return 1;
+    }
+    return staging_release(s, st);
 }
 
 // Stream-ordered collect: the members' counts meet on the device (collect_dyn_kernel), so nothing
@@ -651,10 +697,18 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
     if (t.size == 1) {
         if (nbytes && dst != src && launch_copy(dst, src, nbytes, st)) return 1;
     } else {
-        if (!in_heap(s, dst)) return fail("fcollect: dest must be symmetric-heap memory");
+        if (!device_writable(s, dst)) return fail("fcollect: dest must be heap, device or pinned host memory");
         uint64_t nb[kMaxPes];
         for (int j = 0; j < t.size; ++j) nb[j] = nbytes;
-        if (collect_launch(s, team, dst, src, nb, ret, st)) return 1;
+        // A source outside the heap is staged (every member must pass the same kind of source:
+        // the staged call is several launches).  Zero bytes: only the team synchronises.
+        if (nbytes == 0) {
+            if (team_sync_locked(s, team, st, ret)) return 1;
+        } else if (!in_heap(s, src)) {
+            if (order_stream(s, st) || collect_staged(s, team, (char *) dst, (const char *) src, nb, ret, st)) return 1;
+        } else if (collect_launch(s, team, dst, src, nb, ret, st)) {
+            return 1;
+        }
     }
     if (mark_stream(s, st)) return 1;
     if (blocking) {
@@ -1544,16 +1598,30 @@ int ishmemi_c_collect(int team, void *dest, const void *source, size_t nbytes)
         return fail("collect: invalid team or caller not a member");
     const int p = s.teams[team].size;
     if (p == 1) return ishmemi_c_fcollect(team, dest, source, nbytes);
-    const uint64_t mine = nbytes;
+    // Bit 63 of a count: that member's source is outside the heap; then every member takes the
+    // staged path (peers' sources are only found from a symmetric source address).
+    constexpr uint64_t kStagedBit = 1ull << 63;
+    const uint64_t mine = nbytes | (in_heap(s, source) ? 0 : kStagedBit);
     if (hipMemcpy(s.team_scratch, &mine, 8, hipMemcpyHostToDevice) != hipSuccess)
         return fail("collect: count copy failed");
     if (ishmemi_c_fcollect(team, s.team_scratch + 64, s.team_scratch, 8)) return 1;
     uint64_t counts[kMaxPes];
     if (hipMemcpy(counts, s.team_scratch + 64, 8 * (size_t) p, hipMemcpyDeviceToHost) != hipSuccess)
         return fail("collect: count copy failed");
+    bool staged = false;
+    for (int j = 0; j < p; ++j) {
+        staged = staged || (counts[j] & kStagedBit);
+        counts[j] &= ~kStagedBit;
+    }
     std::lock_guard<std::mutex> lk(s.mu);
-    if (!in_heap(s, dest)) return fail("collect: dest must be symmetric-heap memory");
-    if (collect_launch(s, team, dest, source, counts, nullptr, 0) || mark_stream(s, 0)) return 1;
+    if (!device_writable(s, dest)) return fail("collect: dest must be heap, device or pinned host memory");
+    if (staged) {
+        if (order_stream(s, 0) || collect_staged(s, team, (char *) dest, (const char *) source, counts, nullptr, 0))
+            return 1;
+    } else if (collect_launch(s, team, dest, source, counts, nullptr, 0)) {
+        return 1;
+    }
+    if (mark_stream(s, 0)) return 1;
     HIP_TRY(hipStreamSynchronize(0));
     return check_team_errors(s, team);
 }

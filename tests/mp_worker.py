@@ -892,6 +892,38 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                             fails.append(f"pe{pe} collect {tn} counts{counts_c} so{so} do{do} wrong")
                         ish.ishmem_free(dst_b)
                         ish.ishmem_free(src_b)
+            # Sources outside the heap (the reference's intra-node collect copies from any local
+            # source, collect_impl.h:93-114): staged through the symmetric staging region, in
+            # segments when larger than it (ISHMEM_STAGING_SIZE = 4M here: 5 MiB -> 2 segments);
+            # dest in plain device memory; a collect where only PE 0's source is host memory.
+            for nb_f in (4000, 5 << 20):
+                dsrc = hip.malloc(nb_f)
+                src_pat = oracle.collect_pattern_source(pe, nb_f // 4, 4)
+                hip.upload(dsrc, src_pat)
+                dd = ish.ishmem_malloc(npes * nb_f + 64)
+                want = oracle.collect_check([nb_f // 4] * npes, 4)
+                if ish.ishmem_int32_fcollect(dd, dsrc, nb_f // 4) or not _bits_equal(
+                        hip.download(dd, want.size, np.uint8), want):
+                    fails.append(f"pe{pe} fcollect from device memory {nb_f} B wrong {ish.last_error()}")
+                ddev = hip.malloc(npes * nb_f)
+                if ish.ishmem_int32_fcollect(ddev, dsrc, nb_f // 4) or not _bits_equal(
+                        hip.download(ddev, want.size, np.uint8), want):
+                    fails.append(f"pe{pe} fcollect into device memory {nb_f} B wrong {ish.last_error()}")
+                hip.free(ddev)
+                hip.free(dsrc)
+                ish.ishmem_free(dd)
+            cnts = [int(x) for x in rng.integers(1, 3_000_000, npes)]  # up to 12 MiB: several segments
+            mine_h = np.ascontiguousarray(oracle.collect_pattern_source(pe, cnts[pe], 4))
+            hsrc = ish.ishmem_malloc(cnts[pe] * 4 + 64)
+            hip.upload(hsrc, mine_h)
+            dd = ish.ishmem_malloc(sum(cnts) * 4 + 64)
+            srcp = mine_h.ctypes.data if pe == 0 else hsrc
+            want = oracle.collect_check(cnts, 4)
+            if ish.ishmem_int32_collect(dd, srcp, cnts[pe]) or not _bits_equal(
+                    hip.download(dd, want.size, np.uint8), want):
+                fails.append(f"pe{pe} collect with PE 0's source in host memory wrong {ish.last_error()}")
+            ish.ishmem_free(dd)
+            ish.ishmem_free(hsrc)
             # collect on a stream (ishmemx_<TN>_collect_on_queue): the counts meet on the device.
             # Three calls chained on one stream with no host synchronisation, counts redrawn per
             # call (a count slot reused before a peer read it would show), one member empty,
