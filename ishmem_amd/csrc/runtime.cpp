@@ -1634,6 +1634,31 @@ int ishmemi_c_collect_on_stream(int team, void *dest, const void *source, size_t
 
 int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *source, size_t nelems)
 {
+    // Buffers outside the heap (the reference proxies host buffers to MPI_Scan / MPI_Exscan,
+    // runtime_mpi.cpp:816-835): through symmetric temporaries, copied in / out around the device
+    // scan.  The allocator is deterministic, so members that all pass non-heap buffers of the same
+    // length get temporaries at the same offsets (every member must pass the same kind).
+    State &s = S();
+    char *ts = nullptr, *td = nullptr;
+    const size_t bytes = nelems * dtype_size(dtype);
+    if (s.initialized && nelems && team >= 0 && team < kMaxTeams && s.teams[team].valid &&
+        s.teams[team].size > 1 && (!in_heap(s, dest) || !in_heap(s, source))) {
+        {
+            std::lock_guard<std::mutex> lk(s.mu);
+            ts = in_heap(s, source) ? (char *) source : (char *) heap_alloc(s, bytes, 256);
+            td = in_heap(s, dest) ? (char *) dest : (char *) heap_alloc(s, bytes, 256);
+        }
+        int rc = (!ts || !td) ? 1 : 0;
+        if (!rc && ts != source && hipMemcpy(ts, source, bytes, hipMemcpyDefault) != hipSuccess)
+            rc = fail("scan: staging copy-in failed");
+        if (!rc) rc = scan_impl(team, dtype, inclusive, td, ts, nelems, nullptr, 0, true);
+        if (!rc && td != dest && hipMemcpy(dest, td, bytes, hipMemcpyDefault) != hipSuccess)
+            rc = fail("scan: staging copy-out failed");
+        std::lock_guard<std::mutex> lk(s.mu);
+        if (ts && ts != source) heap_free(s, ts);
+        if (td && td != dest) heap_free(s, td);
+        return rc;
+    }
     return scan_impl(team, dtype, inclusive, dest, source, nelems, nullptr, 0, true);
 }
 

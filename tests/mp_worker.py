@@ -1022,6 +1022,17 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                                      f"{int(np.sum(got.view(np.uint8) != ref.view(np.uint8)))} bytes differ")
                 ish.ishmem_free(d_b)
                 ish.ishmem_free(s_b)
+            # host buffers (the reference proxies them to MPI_Scan / MPI_Exscan): staged through
+            # symmetric temporaries
+            for dt in (DT["int32"], DT["double"]):
+                n = 77_777
+                ins = [oracle.fill_random(dt, 680 + j, n) for j in range(npes)]
+                hs = np.ascontiguousarray(ins[pe])
+                for inc in (True, False):
+                    hd = np.zeros(n, oracle.NP[dt])
+                    r = ish.scan(NAMES[dt], inc, hd.ctypes.data, hs.ctypes.data, n)
+                    if r or not _bits_equal(hd, oracle.scan_fold(dt, ins, pe, inc)):
+                        fails.append(f"pe{pe} host-buffer scan dt{dt} inc={inc} wrong {ish.last_error()}")
             # element-granular path: 4-B aligned (not 16-B) buffers, odd length
             n = 50_001
             ins = [oracle.fill_random(DT["int32"], 650 + j, n) for j in range(npes)]
