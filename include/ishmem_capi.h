@@ -178,6 +178,11 @@ int ishmemi_c_collect_on_stream(int team, void *dest, const void *source, size_t
 int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *source, size_t nelems);
 int ishmemi_c_scan_on_stream(int team, int dtype, int inclusive, void *dest, const void *source,
                              size_t nelems, int *ret, void *stream);
+/* The `deps` / returned-event plumbing of every _on_queue form (fcollect, collect, inscan, exscan;
+ * the reduce has ishmemi_c_reduce_on_stream_deps): make `stream` wait for deps[0..ndeps)
+ * (hipEvent_t), and record `done` (hipEvent_t, may be NULL) on it after the call. */
+int ishmemi_c_stream_wait_events(void *stream, void *const *deps, size_t ndeps);
+int ishmemi_c_stream_record_event(void *stream, void *done);
 
 /* ---- device-initiated collectives ----------------------------------------------------------
  * The reference's device-callable reductions (ishmemx_<TN>_<op>_reduce_work_group,

@@ -127,6 +127,17 @@ inline int ishmemx_fcollectmem_on_stream(void *dest, const void *source, size_t 
     return ishmemx_fcollectmem_on_stream(ISHMEM_TEAM_WORLD, dest, source, nbytes, ret, stream);
 }
 
+namespace ishmemi_cxx {
+/* deps -> call -> done around any stream-ordered call (the reference's _on_queue deps / event). */
+template <typename F>
+inline int with_events(hipStream_t stream, const hipEvent_t *deps, size_t ndeps, hipEvent_t done, F &&call)
+{
+    if (ishmemi_c_stream_wait_events((void *) stream, (void *const *) deps, ndeps)) return 1;
+    if (call()) return 1;
+    return ishmemi_c_stream_record_event((void *) stream, (void *) done);
+}
+}  // namespace ishmemi_cxx
+
 /* collect with per-PE counts on a stream (src/ishmemx.h collectmem / <TN>_collect _on_queue). */
 inline int ishmemx_collectmem_on_stream(ishmem_team_t team, void *dest, const void *source,
                                         size_t nbytes, int *ret, hipStream_t stream)
@@ -196,6 +207,43 @@ inline int ishmemx_collectmem_on_stream(void *dest, const void *source, size_t n
     }
 
 ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_COLL_ON_STREAM, _, _)
+
+/* The same four with the reference's deps / returned event (team form). */
+#define ISHMEMI_CXX_COLL_ON_STREAM_EV(TYPENAME, TYPE, UNUSED1, UNUSED2)                              \
+    inline int ishmemx_##TYPENAME##_fcollect_on_stream(ishmem_team_t team, TYPE *dest,              \
+        const TYPE *source, size_t nelems, int *ret, hipStream_t stream, const hipEvent_t *deps,    \
+        size_t ndeps, hipEvent_t done)                                                             \
+    {                                                                                              \
+        return ishmemi_cxx::with_events(stream, deps, ndeps, done, [&] {                           \
+            return ishmemx_##TYPENAME##_fcollect_on_stream(team, dest, source, nelems, ret, stream); \
+        });                                                                                        \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_collect_on_stream(ishmem_team_t team, TYPE *dest,               \
+        const TYPE *source, size_t nelems, int *ret, hipStream_t stream, const hipEvent_t *deps,    \
+        size_t ndeps, hipEvent_t done)                                                             \
+    {                                                                                              \
+        return ishmemi_cxx::with_events(stream, deps, ndeps, done, [&] {                           \
+            return ishmemx_##TYPENAME##_collect_on_stream(team, dest, source, nelems, ret, stream); \
+        });                                                                                        \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_sum_inscan_on_stream(ishmem_team_t team, TYPE *dest,            \
+        const TYPE *source, size_t nelems, int *ret, hipStream_t stream, const hipEvent_t *deps,    \
+        size_t ndeps, hipEvent_t done)                                                             \
+    {                                                                                              \
+        return ishmemi_cxx::with_events(stream, deps, ndeps, done, [&] {                           \
+            return ishmemx_##TYPENAME##_sum_inscan_on_stream(team, dest, source, nelems, ret, stream); \
+        });                                                                                        \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_sum_exscan_on_stream(ishmem_team_t team, TYPE *dest,            \
+        const TYPE *source, size_t nelems, int *ret, hipStream_t stream, const hipEvent_t *deps,    \
+        size_t ndeps, hipEvent_t done)                                                             \
+    {                                                                                              \
+        return ishmemi_cxx::with_events(stream, deps, ndeps, done, [&] {                           \
+            return ishmemx_##TYPENAME##_sum_exscan_on_stream(team, dest, source, nelems, ret, stream); \
+        });                                                                                        \
+    }
+
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_COLL_ON_STREAM_EV, _, _)
 
 /* Explicit-identity init (the role of ishmemx_init_attr, src/ishmemx.h:21-37). */
 inline int ishmemx_init_pe(int pe, int npes, int device, const char *bootstrap_key)

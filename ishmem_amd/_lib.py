@@ -46,6 +46,8 @@ PROTOTYPES = [
     ("ishmemi_c_fcollect", _i, [_i, _vp, _vp, _sz]),
     ("ishmemi_c_fcollect_on_stream", _i, [_i, _vp, _vp, _sz, _vp, _vp]),
     ("ishmemi_c_collect_on_stream", _i, [_i, _vp, _vp, _sz, _vp, _vp]),
+    ("ishmemi_c_stream_wait_events", _i, [_vp, _vp, _sz]),
+    ("ishmemi_c_stream_record_event", _i, [_vp, _vp]),
     ("ishmemi_c_collect", _i, [_i, _vp, _vp, _sz]),
     ("ishmemi_c_scan", _i, [_i, _i, _i, _vp, _vp, _sz]),
     ("ishmemi_c_scan_on_stream", _i, [_i, _i, _i, _vp, _vp, _sz, _vp, _vp]),

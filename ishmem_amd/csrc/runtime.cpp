@@ -1522,6 +1522,22 @@ int ishmemi_c_reduce_on_stream_deps(int team, int op, int dtype, void *dest, con
     return 0;
 }
 
+int ishmemi_c_stream_wait_events(void *stream, void *const *deps, size_t ndeps)
+{
+    if (ndeps && !deps) return fail("stream_wait_events: deps is NULL with ndeps > 0");
+    for (size_t i = 0; i < ndeps; ++i) {
+        if (!deps[i]) return fail("stream_wait_events: null dependency event");
+        HIP_TRY(hipStreamWaitEvent((hipStream_t) stream, (hipEvent_t) deps[i], 0));
+    }
+    return 0;
+}
+
+int ishmemi_c_stream_record_event(void *stream, void *done)
+{
+    if (done) HIP_TRY(hipEventRecord((hipEvent_t) done, (hipStream_t) stream));
+    return 0;
+}
+
 int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n,
                       void *stream)
 {

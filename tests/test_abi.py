@@ -106,9 +106,11 @@ int main() {
     hipEvent_t deps[1] = {nullptr};
     int r5 = ishmemx_int_sum_reduce_on_stream(ISHMEM_TEAM_WORLD, (int*)nullptr, nullptr, 0, nullptr,
                                               nullptr, deps, 0, nullptr);  // deps / done overload
+    int r7 = ishmemx_int_fcollect_on_stream(ISHMEM_TEAM_WORLD, (int*)nullptr, nullptr, 0, nullptr, nullptr,
+                                            deps, 0, nullptr);  // deps / done form of the collectives
     long *lp = nullptr;
     int r6 = ishmemx_sum_reduce_on_stream(lp, (const long*)lp, 0, nullptr, nullptr);  // generic
-    std::printf("%d %d %d %d %d %d %d\n", r1 != 0, r2 != 0, r3 != 0, r4 != 0, r5 != 0, r6 != 0, ishmem_my_pe());
+    std::printf("%d %d %d %d %d %d %d %d\n", r1 != 0, r2 != 0, r3 != 0, r4 != 0, r5 != 0, r6 != 0, r7 != 0, ishmem_my_pe());
     return 0;
 }
 ''')
@@ -118,7 +120,7 @@ int main() {
                    check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, out.stderr
-    assert out.stdout.split() == ["1", "1", "1", "1", "1", "1", "-1"]
+    assert out.stdout.split() == ["1", "1", "1", "1", "1", "1", "1", "-1"]
 
 
 def test_c_header_is_plain_c(tmp_path):
