@@ -220,7 +220,8 @@ void *ishmemi_c_device_ctx(void);
  * multi-PE call: init agrees on them (minimum over the PEs) and a later set_param must be made
  * with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,
  * nothing is paired by workgroup index).  ishmemi_c_get_param also reports "staging_bytes",
- * "heap_bytes", "flags_fine_grained" and "cu_count" (compute units of this PE's device). */
+ * "heap_bytes", "flags_fine_grained", "cu_count" (compute units of this PE's device) and
+ * "device_share" (PEs of the job on this PE's device: 1 with one PE per GPU). */
 const char *ishmemi_c_last_error(void);
 int ishmemi_c_set_param(const char *name, long long value);
 long long ishmemi_c_get_param(const char *name);

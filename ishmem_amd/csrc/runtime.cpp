@@ -1722,6 +1722,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "flags_kind") return s.flags_kind;
     if (n == "staging_bytes") return (long long) s.staging_bytes;
     if (n == "heap_bytes") return (long long) s.heap_size;
+    if (n == "device_share") return device_share();  // PEs of the job on this PE's device
     if (n == "launch_words") return (long long) (uintptr_t) s.kern_ep;  // debug: device address
     if (n == "cu_count") {
         int dev = 0, cus = 0;

@@ -17,6 +17,151 @@ from __future__ import annotations
 
 import numpy as np
 
+# ---- rotating-winner input pattern for the large-size parity checks ---------------------------
+# Used by bench.py's every-word check and by the GPU tests at BASELINE's sizes (configs[2..4]),
+# where an oracle fold of p full arrays would not fit the time budget.  Element i of PE pe:
+#     x_pe[i] = 1 + h(i) + 1024 * ((i + pe) mod p),   h(i) = mix32(i) >> 22  (0..1023)
+# h is a bijective 32-bit mixer of the full element index (its high word folded in), so no two
+# 16 KiB tiles, segments or 4 GiB windows hold the same bytes; the high part gives every PE a
+# different value at every index and rotates the min / max winner over all p PEs, so a fold that
+# skips or duplicates a member changes the result.  Values stay below 1024 * (p + 1): sums are
+# exact in f32 / f64 / int32, int32 products wrap, f64 products are folded in team order (the
+# order the kernels use) when the expected value is formed.  (Round 2 used (i mod 1024) + pe: one
+# period per 16 KiB tile, identical bytes in every tile, the min / max always from PEs 0 / p-1.)
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def _mix32(x: np.ndarray) -> np.ndarray:
+    """lowbias32 (bijective on uint32), in place on a uint32 array."""
+    x ^= x >> np.uint32(16)
+    x *= np.uint32(0x7FEB352D)
+    x ^= x >> np.uint32(15)
+    x *= np.uint32(0x846CA68B)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def _pieces(lo: int, m: int):
+    """Split [lo, lo + m) at multiples of 2^32: (offset in output, low words, high word)."""
+    off = 0
+    while off < m:
+        i = lo + off
+        hi = i >> 32
+        take = min(m - off, ((hi + 1) << 32) - i)
+        yield off, np.arange(i & 0xFFFFFFFF, (i & 0xFFFFFFFF) + take, dtype=np.uint32), hi
+        off += take
+
+
+def _hash_lo(lo32: np.ndarray, hi: int) -> np.ndarray:
+    """h over one 2^32-aligned piece (consumes lo32)."""
+    if hi:
+        lo32 ^= _mix32(np.array([(hi * 0x9E3779B9 + 0x632BE5AB) & 0xFFFFFFFF], np.uint32))[0]
+    h = _mix32(lo32)
+    h >>= np.uint32(22)
+    return h
+
+
+def _rot_lo(lo32: np.ndarray, hi: int, shift: int, p: int) -> np.ndarray:
+    """(i + shift) mod p over one piece, as uint32 (p <= 64)."""
+    c = ((hi << 32) + shift) % p
+    if p & (p - 1) == 0:  # p divides 2^32: wrapping adds keep the residue
+        x = lo32 + np.uint32(c)
+        x &= np.uint32(p - 1)
+        return x
+    x = lo32 % np.uint32(p)
+    x += np.uint32(c)
+    x[x >= p] -= np.uint32(p)
+    return x
+
+
+def pattern_hash(lo: int, m: int) -> np.ndarray:
+    """h(i) for i in [lo, lo + m): 10-bit hash of the full 64-bit index (uint32 array)."""
+    out = np.empty(m, np.uint32)
+    for off, lo32, hi in _pieces(lo, m):
+        out[off:off + len(lo32)] = _hash_lo(lo32, hi)
+    return out
+
+
+_SUB = 1 << 20  # elements per internal block: temporaries stay cache-sized (no page faults)
+
+
+def _blocks(lo: int, m: int):
+    for a in range(0, m, _SUB):
+        yield a, lo + a, min(_SUB, m - a)
+
+
+def _pattern_into(out: np.ndarray, pe: int, p: int, lo: int) -> None:
+    for off, lo32, hi in _pieces(lo, len(out)):
+        x = _rot_lo(lo32, hi, pe, p)
+        x *= np.uint32(1024)
+        x += _hash_lo(lo32, hi)
+        x += np.uint32(1)
+        out[off:off + len(x)] = x
+
+
+def pattern(pe: int, p: int, lo: int, m: int, npd) -> np.ndarray:
+    """x_pe[lo : lo + m] of the rotating-winner pattern, as dtype npd."""
+    out = np.empty(m, npd)
+    for a, b, k in _blocks(lo, m):
+        _pattern_into(out[a:a + k], pe, p, b)
+    return out
+
+
+def _expected_block(op: str, npd, p: int, lo: int, m: int) -> np.ndarray:
+    h = pattern_hash(lo, m)
+    if op == "sum":  # {(i + pe) mod p : pe} is 0..p-1 at every i
+        h += np.uint32(1)
+        if p * 1024 * (p + 1) < (1 << 31):
+            h *= np.uint32(p)
+            h += np.uint32(1024 * p * (p - 1) // 2)
+            return h.astype(npd)
+        return (np.uint64(p) * h.astype(np.uint64) + np.uint64(1024 * p * (p - 1) // 2)).astype(npd)
+    if op == "min":
+        h += np.uint32(1)
+        return h.astype(npd)
+    if op == "max":
+        h += np.uint32(1 + 1024 * (p - 1))
+        return h.astype(npd)
+    if op == "prod":
+        if np.issubdtype(np.dtype(npd), np.integer):  # wraps mod 2^32, order-independent
+            acc = np.ones(m, np.uint32)
+            for pe in range(p):
+                acc *= pattern(pe, p, lo, m, np.uint32)
+            return acc.view(np.int32).astype(npd) if np.dtype(npd).itemsize == 4 else acc.astype(npd)
+        acc = pattern(0, p, lo, m, npd)
+        for pe in range(1, p):
+            acc *= pattern(pe, p, lo, m, npd)  # team order, like the kernels
+        return acc
+    raise ValueError(f"pattern_expected: unsupported op {op}")
+
+
+def pattern_expected(op: str, npd, p: int, lo: int, m: int) -> np.ndarray:
+    """The team-order fold over PEs 0..p-1 of pattern() at [lo, lo + m)."""
+    out = np.empty(m, npd)
+    for a, b, k in _blocks(lo, m):
+        out[a:a + k] = _expected_block(op, npd, p, b, k)
+    return out
+
+
+def upload_pattern(hip, ptr: int, npd, pe: int, p: int, n: int, chunk: int = 1 << 26) -> None:
+    """dest[0:n] = pattern(pe, p, ...), uploaded in chunks (no n-sized host temporaries)."""
+    es = np.dtype(npd).itemsize
+    for lo in range(0, n, chunk):
+        m = min(chunk, n - lo)
+        hip.upload(ptr + lo * es, pattern(pe, p, lo, m, npd))
+
+
+def count_wrong(hip, ptr: int, op: str, npd, p: int, lo: int, m: int, chunk: int = 1 << 26) -> int:
+    """Bytes of dest[lo : lo + m] (device) that differ from pattern_expected."""
+    es = np.dtype(npd).itemsize
+    bad = 0
+    for a in range(lo, lo + m, chunk):
+        k = min(chunk, lo + m - a)
+        want = pattern_expected(op, npd, p, a, k)
+        got = hip.download(ptr + a * es, k, npd)
+        bad += int(np.count_nonzero(got.view(np.uint8) != want.view(np.uint8)))
+    return bad
+
 
 def _base(pe: int, n: int) -> np.ndarray:
     # Deterministic full-range int32 words per PE (xorshift-multiply hash of the index).

@@ -30,6 +30,8 @@ for s in $STEPS; do
   case "$s" in
     smoke)  run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
     gpu)    run pytest_gpu 1500 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider ;;
+    sel)    run pytest_sel ${SEL_SECS:-1500} python -u -m pytest tests -m gpu -x -v --timeout ${SEL_TIMEOUT:-900} \
+                --timeout-method thread -p no:cacheprovider -k "$SEL" ;;
     single) run pytest_single 900 python -m pytest tests/test_gpu_single.py -m gpu -x -q -p no:cacheprovider ;;
     multi)  run pytest_multi 1200 python -m pytest tests/test_gpu_multi.py -m gpu -x -q -p no:cacheprovider ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;

@@ -18,35 +18,6 @@ import numpy as np
 GOLDEN = Path(__file__).resolve().parent / "golden"
 
 
-def closed_form(op: str, npd, npes: int, idx: np.ndarray) -> np.ndarray:
-    """Reduce over PEs of x_pe[i] = (i mod 1024) + pe (exact in every type: int32 prod wraps,
-    f64 prod of <= 8 factors below 2^10 each is exact)."""
-    base = idx % 1024
-    if op == "min":
-        return base.astype(npd)
-    if op == "max":
-        return (base + npes - 1).astype(npd)
-    if op == "sum":
-        return (base * npes + npes * (npes - 1) // 2).astype(npd)
-    if npd is np.float64:
-        acc = base.astype(np.float64)
-        for pe in range(1, npes):
-            acc = acc * (base.astype(np.float64) + pe)
-        return acc
-    acc = base.astype(np.uint32)
-    for pe in range(1, npes):
-        acc = (acc * (base + pe).astype(np.uint32)).astype(np.uint32)
-    return acc.view(np.int32)
-
-
-def upload_closed_form(hip, ptr: int, npd, pe: int, n: int, chunk: int = 1 << 26) -> None:
-    """x_pe[i] = (i mod 1024) + pe, uploaded in chunks (no n-sized host temporaries)."""
-    for lo in range(0, n, chunk):
-        m = min(chunk, n - lo)
-        x = ((np.arange(lo, lo + m, dtype=np.int64) % 1024) + pe).astype(npd)
-        hip.upload(ptr + lo * np.dtype(npd).itemsize, x)
-
-
 def _bits_equal(a, b):
     return np.array_equal(np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8))
 
@@ -548,25 +519,21 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
 
         if "huge" in scenarios:
             # > 2 GiB per PE with a misaligned start and an odd length: the head, the tail and the
-            # 2 GiB descriptor-range boundary are all exercised.  x_pe[i] = (i mod 1024) + pe, so
-            # the exact sum is known in closed form.
+            # 2 GiB descriptor-range boundary are all exercised.  Rotating-winner pattern
+            # (selfcheck.pattern: non-periodic, every PE distinct), every word compared.
+            from ishmem_amd import selfcheck as sc
             n = (1 << 29) + (1 << 27) + 5  # 2.5 GiB + 20 B of float32
             s_base = ish.ishmem_malloc(n * 4 + 64)
             d_base = ish.ishmem_malloc(n * 4 + 64)
             s, d = s_base + 4, d_base + 4
-            x = (np.arange(n, dtype=np.int64) % 1024).astype(np.float32) + np.float32(pe)
-            hip.upload(s, x)
-            del x
+            sc.upload_pattern(hip, s, np.float32, pe, npes, n)
             r = ish.ishmem_float_sum_reduce(d, s, n)
             if r:
                 fails.append(f"pe{pe} huge rc={r} {ish.last_error()}")
             else:
-                for lo in (0, (1 << 29) - 7, n - 40):
-                    got = hip.download(d + lo * 4, 40, np.float32)
-                    i = np.arange(lo, lo + 40)
-                    exp = (i % 1024).astype(np.float32) * npes + np.float32(npes * (npes - 1) / 2)
-                    if not np.array_equal(got, exp):
-                        fails.append(f"pe{pe} huge: wrong values near element {lo}")
+                bad = sc.count_wrong(hip, d, "sum", np.float32, npes, 0, n)
+                if bad:
+                    fails.append(f"pe{pe} huge: {bad} of {4 * n} bytes wrong")
             ish.ishmem_free(d_base)
             ish.ishmem_free(s_base)
 
@@ -794,33 +761,69 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             if not res["checked"]:
                 fails.append(f"pe{pe} tripwire: {res}")
 
-        if "cfg4" in scenarios:
-            # BASELINE configs[3] at its own size: float32 sum-reduce of 1 GiB per PE, every word of
-            # dest compared with the closed form on every PE.
+        if "cfg3" in scenarios or "cfg4" in scenarios:
+            # BASELINE configs[2] (2 PEs) / configs[3] (8 PEs) at their own size: float32 sum-reduce
+            # of 1 GiB per PE, every word of dest compared on every PE with the team-order fold of
+            # the rotating-winner pattern (selfcheck.pattern).
+            from ishmem_amd import selfcheck as sc
             n = 256 << 20
             s, d = ish.ishmem_malloc(n * 4), ish.ishmem_malloc(n * 4)
             if not (s and d):
-                raise RuntimeError(f"cfg4 heap: {ish.last_error()}")
-            upload_closed_form(hip, s, np.float32, pe, n)
+                raise RuntimeError(f"cfg3/4 heap: {ish.last_error()}")
+            sc.upload_pattern(hip, s, np.float32, pe, npes, n)
+            hip.memset(d, 0xFF, n * 4)
             r = ish.ishmem_float_sum_reduce(d, s, n)
             if r:
-                fails.append(f"pe{pe} cfg4 rc={r} {ish.last_error()}")
+                fails.append(f"pe{pe} cfg3/4 rc={r} {ish.last_error()}")
             else:
-                bad = 0
-                for lo in range(0, n, 1 << 26):
-                    m = min(1 << 26, n - lo)
-                    want = closed_form("sum", np.float32, npes, np.arange(lo, lo + m, dtype=np.int64))
-                    bad += int(np.count_nonzero(hip.download(d + 4 * lo, m, np.float32) != want))
+                bad = sc.count_wrong(hip, d, "sum", np.float32, npes, 0, n)
                 if bad:
-                    fails.append(f"pe{pe} cfg4: {bad} of {n} words wrong")
+                    fails.append(f"pe{pe} cfg3/4: {bad} of {4 * n} bytes wrong")
+                elif pe == 0:
+                    print(f"[cfg] pe0: {npes} PEs x 1 GiB f32 sum, every word matches", flush=True)
             ish.ishmem_free(d)
             ish.ishmem_free(s)
 
+        if "cfg1" in scenarios:
+            # BASELINE configs[0]: int32 sum-reduce over HOST buffers (the reference's host path,
+            # reduce_impl.h:301-315), full-range seeded int32 (oracle.fill_random), n from the
+            # examples/5_pi_reduce.cpp single element to 16 Mi; pageable (numpy) and pinned
+            # buffers, in place and not; bit-exact vs the oracle fold on every PE.
+            for n in (1, 1 << 10, (1 << 16) + 3, 1 << 20, 16 << 20):
+                ins = [oracle.fill_random(DT["int32"], 0x15AE0001 + j, n) for j in range(npes)]
+                src = np.ascontiguousarray(ins[pe])
+                out = np.zeros(n, np.int32)
+                r = ish.ishmem_int32_sum_reduce(out.ctypes.data, src.ctypes.data, n)
+                if r:
+                    fails.append(f"pe{pe} cfg1 pageable n={n} rc={r} {ish.last_error()}")
+                else:
+                    check(f"cfg1 pageable n={n}", OPS["sum"], DT["int32"], ins, out)
+                hin, hout = hip.host_malloc(n * 4), hip.host_malloc(n * 4)
+                hv = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_int32 * n).from_address(hin))
+                hv[:] = ins[pe]
+                r = ish.ishmem_int_sum_reduce(hout, hin, n)
+                got = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_int32 * n).from_address(hout)).copy()
+                if r:
+                    fails.append(f"pe{pe} cfg1 pinned n={n} rc={r} {ish.last_error()}")
+                else:
+                    check(f"cfg1 pinned n={n}", OPS["sum"], DT["int32"], ins, got)
+                r = ish.ishmem_int_sum_reduce(hin, hin, n)  # in place on host memory
+                got = hv.copy()
+                if r:
+                    fails.append(f"pe{pe} cfg1 pinned in place n={n} rc={r} {ish.last_error()}")
+                else:
+                    check(f"cfg1 pinned in place n={n}", OPS["sum"], DT["int32"], ins, got)
+                del hv
+                hip.host_free(hin)
+                hip.host_free(hout)
+
         if "cfg5" in scenarios:
             # BASELINE configs[4]: min / max / prod x int32 / float64 at 4 KiB * 4^k up to
-            # CFG5_MAX_BYTES (4 GiB) per PE.  Up to 64 MiB every word is compared; above, windows
-            # of 4096 elements at both edges of every member's chunk, the array's end and 16
-            # seeded random places (int: bit-exact; f64 min / max / prod of small integers: exact).
+            # CFG5_MAX_BYTES (4 GiB) per PE, rotating-winner pattern (selfcheck.pattern).  Up to
+            # 64 MiB every word is compared; above, windows of 4096 elements at both edges of every
+            # member's chunk, the array's end and 16 seeded random places (int: bit-exact; f64
+            # min / max exact, prod folded in team order like the kernels: bit-exact).
+            from ishmem_amd import selfcheck as sc
             maxb = int(os.environ.get("CFG5_MAX_BYTES", 4 << 30))
             rng = np.random.default_rng(55)
             for dtn, npd in (("int32", np.int32), ("double", np.float64)):
@@ -829,7 +832,7 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 s, d = ish.ishmem_malloc(maxb), ish.ishmem_malloc(maxb)
                 if not (s and d):
                     raise RuntimeError(f"cfg5 heap: {ish.last_error()}")
-                upload_closed_form(hip, s, npd, pe, nmax)
+                sc.upload_pattern(hip, s, npd, pe, npes, nmax)
                 for op in ("min", "max", "prod"):
                     nb = 4096
                     while nb <= maxb:
@@ -852,11 +855,7 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                                     wins.append((lo, min(n, lo + 4096) - lo))
                             wins.append((n - 4096, 4096))
                             wins += [(int(x), 4096) for x in rng.integers(0, n - 4096, 16)]
-                        bad = 0
-                        for lo, m in wins:
-                            want = closed_form(op, npd, npes, np.arange(lo, lo + m, dtype=np.int64))
-                            got = hip.download(d + lo * es, m, npd)
-                            bad += int(np.count_nonzero(got.view(np.uint8) != want.view(np.uint8)))
+                        bad = sum(sc.count_wrong(hip, d, op, npd, npes, lo, m) for lo, m in wins)
                         if bad:
                             fails.append(f"pe{pe} cfg5 {op} {dtn} {nb} B: {bad} bytes wrong")
                         nb *= 4

@@ -23,3 +23,40 @@ def test_bench_self_launches_ranks_and_relays_one_json_line():
         assert r.returncode != 0
     else:
         assert r.returncode == 0 and d["value"] > 0 and "algbw_GiBps" in d
+
+
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_roofline_same_device_is_hbm_bound_and_at_most_one():
+    # Round-2 rehearsal numbers: 2 PEs on one GPU, 1 GiB each, 1.0 ms per launch.  Against the
+    # xGMI spec this read 6.17x "peak"; against the device's HBM it is a fraction below 1.
+    b = _bench()
+    B = 1 << 30
+    roof, t_roof = b.roofline(2, 2, B, 1.0)
+    assert roof["bound"] == "hbm" and roof["pes_per_device"] == 2
+    assert abs(roof["achieved"] - 2 * 2.5 * B / 1e-3 / 1e9) < 1e-6
+    assert 0 < roof["frac"] <= 1 and "model_violated" not in roof
+    assert roof["traffic"] is not None  # committed same-device PMC entry (profiles/pmc_summary.json)
+    assert B / t_roof >= B / 1e-3  # the step cannot beat its roofline
+    roof8, _ = b.roofline(8, 8, B, 4.5)
+    assert roof8["bound"] == "hbm" and roof8["frac"] <= 1
+
+
+def test_roofline_one_pe_per_gpu_is_xgmi_and_flags_a_violated_model():
+    b = _bench()
+    B = 1 << 30
+    roof, t_roof = b.roofline(8, 1, B, 2.0)  # 1.75 GiB of ingress per PE in 2 ms
+    assert roof["bound"] == "xgmi" and roof["peak"] == b.XGMI_LINK_GBS * 7
+    assert roof["traffic"] is None and "traffic_note" in roof
+    assert 0 < roof["frac"] <= 1
+    fast, _ = b.roofline(2, 1, B, 1.0)  # faster than the per-link spec allows
+    assert fast["frac"] is None and fast["model_violated"] and fast["frac_raw"] > 1 and fast["reason"]
+    one, t1 = b.roofline(1, 1, B, 0.3174)
+    assert one["bound"] == "hbm" and abs(one["frac"] - 2 * B / 0.3174e-3 / 1e9 / 8000) < 1e-9
+    assert abs(t1 - 2 * B / 8e12) < 1e-12

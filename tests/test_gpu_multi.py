@@ -145,6 +145,22 @@ def test_config4_eight_pes_1GiB_f32_sum_full_compare():
     run_pes(8, ["cfg4"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "3G"}, timeout=600)
 
 
+@pytest.mark.parametrize("oneshot", ["default", "rs_ag"])
+def test_config3_two_pes_1GiB_f32_sum_full_compare(oneshot):
+    # BASELINE configs[2]: 2 PEs x 1 GiB f32 sum, every word compared on both PEs (rotating-winner
+    # pattern); the default two-member kernel and forced reduce-scatter + all-gather.
+    env = {"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "3G"}
+    if oneshot == "rs_ag":
+        env["ISHMEM_ONESHOT_P2_MAX_BYTES"] = 0
+    run_pes(2, ["cfg3"], env=env, timeout=400)
+
+
+def test_config1_two_pes_int32_sum_host_buffers():
+    # BASELINE configs[0]: int32 sum over host buffers (pageable and pinned, in place and not),
+    # 2 PEs, 1 .. 16 Mi elements, bit-exact vs the oracle.
+    run_pes(2, ["cfg1"], env={"ISHMEM_MAX_BLOCKS": 256}, timeout=300)
+
+
 @pytest.mark.parametrize("npes", [2, 8])
 def test_config5_min_max_prod_int32_f64_4KiB_to_4GiB(npes):
     # BASELINE configs[4]: min/max/prod x int32/float64, 4 KiB * 4^k up to 4 GiB per PE, every
