@@ -1,43 +1,58 @@
-/* ishmem_amd — device-callable (work-group) reductions, header-only HIP.
+/* ishmem_amd — device-callable collectives, header-only HIP (included by ishmem.h / ishmemx.h
+ * when the translation unit is compiled as HIP, so a kernel sees the reference's device API).
  *
- * Analogue of the reference's
- *   template <typename Group> int ishmemx_<TYPENAME>_<op>_reduce_work_group([team,] TYPE *dest,
- *                                  const TYPE *source, size_t nreduce, const Group &grp)
- * (src/ishmemx.h:1648-1699, src/collectives/reduce_impl.h:386-418, :505-518): called by EVERY
- * thread of ONE work-group on every PE of the team, from inside a user kernel.  The library state
- * is passed explicitly (`ctx` = ishmemi_c_device_ctx(), handed to the kernel as an argument),
- * because a HIP user kernel cannot see the library's device globals the way SYCL's do.
+ * Analogue of the reference's SYCL_EXTERNAL device API, called exactly as the reference calls it:
+ *   ishmemx_<TYPENAME>_<op>_reduce_work_group([team,] dest, source, nreduce, grp)
+ *       (src/ishmemx.h:1209-1803, src/collectives/reduce_impl.h:386-418, :505-518) — every thread
+ *       of the group `grp` calls, on every PE of the team;
+ *   ishmem_<TYPENAME>_<op>_reduce([team,] dest, source, nreduce) from ONE work-item (the
+ *       reference's device-side blocking call, e.g. in a single_task: examples/6_team_split_strided.cpp:67);
+ *   fcollect / collect / sum_inscan / sum_exscan / broadcast in the same forms;
+ *   ishmem_my_pe / n_pes / team_my_pe / team_n_pes / team_translate_pe / ptr / info_get_*,
+ *   ishmem_barrier_all / sync_all / team_sync and their *_work_group forms, ishmemx_print.
+ * `grp` is a HIP cooperative group — cooperative_groups::thread_block (the reference's
+ * sycl::group) or a 64-lane cooperative_groups::thread_block_tile (its sycl::sub_group) — or one of
+ * the tags ishmemx_dev::work_group / wavefront.
  *
- *   __global__ void k(const ishmemi_c_device_ctx_t *ctx, float *dst, const float *src, size_t n) {
+ *   __global__ void k(int *dst, const int *src, size_t n) {
+ *       auto grp = cooperative_groups::this_thread_block();
  *       ... produce src ...
- *       int rc = ishmemx_float_sum_reduce_work_group(ctx, dst, src, n);
+ *       int rc = ishmemx_int_sum_reduce_work_group(dst, src, n, grp);
  *   }
  *
- * The trailing group argument selects who calls: `ishmemx_dev::work_group` (default, every
- * thread of the work-group) or `ishmemx_dev::wavefront` (one full 64-lane wavefront — the
- * reference's sycl::sub_group overload).  The device-side blocking call of the reference
- * (`ishmem_<TYPENAME>_<op>_reduce` from inside a kernel, e.g. in a single_task) is
- * `ishmem_<TYPENAME>_<op>_reduce(ctx, [team,] dest, source, nreduce)` called by ONE work-item.
+ * The library's device state reaches the kernel without an argument: every translation unit
+ * that includes this header owns a device pointer to the library's context and registers it with
+ * the library from a static initializer; ishmem_init fills every registered copy (a code object
+ * loaded later is filled when it registers).  This is what SYCL device globals give the reference.
  *
  * Algorithm: the same direct reduce-scatter + all-gather as the host-launched kernel, executed by
- * the calling work-group (member c folds chunk c of every member's source in canonical team order
+ * the calling group (member c folds chunk c of every member's source in canonical team order
  * with system-coherent loads, stores it write-through, team barrier, then pulls the other chunks).
- * `source` must have been written by the calling work-group or by earlier kernels (the start
- * barrier releases this work-group's own writes).  Returns 0, or nonzero if a peer did not arrive
- * within the library's timeout.  dest/source must be symmetric-heap addresses.
+ * `source` must have been written by the calling group or by earlier kernels (the start barrier
+ * releases this group's own writes).  Returns 0, or nonzero if the library is not initialised or
+ * a peer did not arrive within the library's timeout.  dest/source must be symmetric-heap
+ * addresses; source and dest identical or disjoint (reduce), disjoint (scan, collect).
  */
 #ifndef ISHMEM_AMD_ISHMEMX_DEVICE_H
 #define ISHMEM_AMD_ISHMEMX_DEVICE_H
 
+#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include <type_traits>
 
 #include "ishmem_capi.h"
 
 namespace ishmemx_dev {
+
+// This translation unit's pointer to the library's device context (see the header comment).
+static __device__ const ishmemi_c_device_ctx_t *g_ctx = nullptr;
+[[maybe_unused]] static const int g_ctx_registered = ishmemi_c_register_device_ctx_slot((const void *) &g_ctx);
+
+__device__ __forceinline__ const ishmemi_c_device_ctx_t *ctx() { return g_ctx; }
 
 template <typename T, int OP>
 __device__ __forceinline__ T op1(T a, T b)
@@ -159,6 +174,26 @@ struct thread_t {  // one work-item (device-side ishmem_<TN>_<op>_reduce)
 inline constexpr work_group_t work_group{};
 inline constexpr wavefront_t wavefront{};
 inline constexpr thread_t thread{};
+
+// Group argument -> execution tag: the library's tags, and HIP cooperative groups in the roles of
+// the reference's sycl::group (thread_block) and sycl::sub_group (a 64-lane tile).
+template <typename G>
+struct exec_of {
+    static_assert(std::is_same_v<G, work_group_t> || std::is_same_v<G, wavefront_t> || std::is_same_v<G, thread_t>,
+                  "group: cooperative_groups::thread_block, thread_block_tile<64>, or an ishmemx_dev tag");
+    using type = G;
+};
+template <>
+struct exec_of<cooperative_groups::thread_block> {
+    using type = work_group_t;
+};
+template <unsigned N, typename P>
+struct exec_of<cooperative_groups::thread_block_tile<N, P>> {
+    static_assert(N == 64, "a sub-group collective needs the whole 64-lane wavefront (thread_block_tile<64>)");
+    using type = wavefront_t;
+};
+template <typename G>
+using exec_t = typename exec_of<std::remove_cv_t<std::remove_reference_t<G>>>::type;
 
 // Team barrier among the calling groups (one per member): the group's leader stores the epoch
 // into its slot of every peer's row and polls its own row; bounded by the library timeout.
@@ -388,7 +423,10 @@ __device__ inline int scan_group(const ishmemi_c_device_ctx_t *c, int team, T *d
 {
     const int tid = G::rank(), nthr = G::size();
     const int size = c->team_size[team], me = c->team_my_idx[team];
-    if (size <= 0 || me < 0 || (size > 1 && dest == source)) return 1;
+    // dest and source must be disjoint: a peer may still be reading this PE's source.
+    const bool overlap = (const char *) dest < (const char *) (source + nelems) &&
+                         (const char *) source < (const char *) (dest + nelems);
+    if (size <= 0 || me < 0 || (size > 1 && nelems && overlap)) return 1;
     const uint32_t epoch = group_epoch<G>(c, team);
     if (size > 1 && !group_barrier<G>(c, team, 0, epoch, true)) return 1;
     const int last = inclusive ? me : me - 1;
@@ -429,6 +467,48 @@ __device__ inline int scan_group(const ishmemi_c_device_ctx_t *c, int team, T *d
         G::sync();
         return 0;
     }
+    return group_barrier<G>(c, team, 2, epoch, false) ? 0 : 1;
+}
+
+// Team barrier from inside a kernel (ishmem_team_sync / sync_all / barrier_all and their
+// *_work_group forms, src/collectives/sync_impl.h:30-69): the group's writes are released, then
+// every member's group meets on the team's phase-3 row.  There is no RMA in this library, so
+// barrier_all's quiet has nothing further to complete.
+template <typename G>
+__device__ inline int team_sync_group(const ishmemi_c_device_ctx_t *c, int team)
+{
+    if (!c || team < 0 || team >= ISHMEMI_C_MAX_TEAMS) return 1;
+    const int size = c->team_size[team], me = c->team_my_idx[team];
+    if (size <= 0 || me < 0) return 1;
+    if (size == 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        G::sync();
+        return 0;
+    }
+    const uint32_t epoch = group_epoch<G>(c, team);
+    return group_barrier<G>(c, team, 3, epoch, true) ? 0 : 1;
+}
+
+// Broadcast (src/collectives/broadcast_impl.h, its intra-node pull variant): start barrier (the
+// root's source is final), every member including the root pulls `nbytes` of the root's source
+// into its dest, end barrier (the root may reuse its source).
+template <typename G>
+__device__ inline int broadcast_group(const ishmemi_c_device_ctx_t *c, int team, void *dest,
+                                      const void *source, size_t nbytes, int root)
+{
+    if (!c || team < 0 || team >= ISHMEMI_C_MAX_TEAMS) return 1;
+    const int size = c->team_size[team], me = c->team_my_idx[team];
+    if (size <= 0 || me < 0 || root < 0 || root >= size) return 1;
+    const uint32_t epoch = group_epoch<G>(c, team);
+    if (size == 1) {
+        if (dest != source) group_copy<G>((const char *) source, (char *) dest, nbytes, false);
+        G::sync();
+        return 0;
+    }
+    if (!group_barrier<G>(c, team, 0, epoch, true)) return 1;
+    const int groot = c->team_start[team] + root * c->team_stride[team];
+    if (root != me) group_copy<G>(peer_addr(c, source, groot), (char *) dest, nbytes, true);
+    else if (dest != source) group_copy<G>((const char *) source, (char *) dest, nbytes, false);
     return group_barrier<G>(c, team, 2, epoch, false) ? 0 : 1;
 }
 
