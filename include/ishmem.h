@@ -23,14 +23,43 @@
 
 #include "ishmem_capi.h"
 
+/* ---- version, threading (src/ishmem.h:17-26) ---------------------------------------------- */
+#define ISHMEM_MAJOR_VERSION ISHMEMI_C_SPEC_MAJOR
+#define ISHMEM_MINOR_VERSION ISHMEMI_C_SPEC_MINOR
+#define ISHMEM_PATCH_VERSION ISHMEMI_C_SPEC_PATCH
+#define ISHMEM_MAX_NAME_LEN  ISHMEMI_C_MAX_NAME_LEN
+#define ISHMEM_VENDOR_STRING ISHMEMI_C_VENDOR_STRING
+
+#define ISHMEM_THREAD_SINGLE     ISHMEMI_C_THREAD_SINGLE
+#define ISHMEM_THREAD_FUNNELED   ISHMEMI_C_THREAD_FUNNELED
+#define ISHMEM_THREAD_SERIALIZED ISHMEMI_C_THREAD_SERIALIZED
+#define ISHMEM_THREAD_MULTIPLE   ISHMEMI_C_THREAD_MULTIPLE
+
 typedef int ishmem_team_t; /* src/ishmem.h:61 */
+typedef struct {           /* src/ishmem.h:63-65 */
+    int num_contexts;
+} ishmem_team_config_t;
+#define ISHMEM_TEAM_NUM_CONTEXTS 1L
 #define ISHMEM_TEAM_INVALID ISHMEMI_C_TEAM_INVALID
 #define ISHMEM_TEAM_WORLD   ISHMEMI_C_TEAM_WORLD
 #define ISHMEM_TEAM_SHARED  ISHMEMI_C_TEAM_SHARED
 
-/* ---- setup (src/ishmem.h:40-56) ---------------------------------------------------------- */
+/* ---- setup (src/ishmem.h:40-58) ---------------------------------------------------------- */
 inline void ishmem_init(void) { (void) ishmemi_c_init(); }
 inline void ishmem_finalize(void) { (void) ishmemi_c_finalize(); }
+inline int ishmem_init_thread(int requested, int *provided) { return ishmemi_c_init_thread(requested, provided); }
+inline void ishmem_query_thread(int *provided) { (void) ishmemi_c_query_thread(provided); }
+inline void ishmem_info_get_version(int *major, int *minor)
+{
+    *major = ISHMEM_MAJOR_VERSION;
+    *minor = ISHMEM_MINOR_VERSION;
+}
+inline void ishmem_info_get_name(char *name)
+{
+    const char *v = ISHMEM_VENDOR_STRING;
+    while (*v) *name++ = *v++;
+    *name = '\0';
+}
 inline int ishmem_my_pe(void) { return ishmemi_c_my_pe(); }
 inline int ishmem_n_pes(void) { return ishmemi_c_n_pes(); }
 inline void *ishmem_malloc(size_t size) { return ishmemi_c_malloc(size); }
@@ -46,20 +75,33 @@ inline int ishmem_team_translate_pe(ishmem_team_t src_team, int src_pe, ishmem_t
 {
     return ishmemi_c_team_translate_pe(src_team, src_pe, dest_team);
 }
-/* The reference's config/config_mask arguments (src/ishmem.h:79-85) are accepted and ignored:
- * no team configuration option affects reductions. */
+/* The config / config_mask arguments (src/ishmem.h:78-85): the only option, num_contexts, is
+ * stored on the new team and reported by ishmem_team_get_config (contexts do not exist on this
+ * path; nothing else depends on it). */
+inline int ishmem_team_get_config(ishmem_team_t team, long config_mask, ishmem_team_config_t *config)
+{
+    return ishmemi_c_team_get_config(team, config_mask, config ? &config->num_contexts : (int *) 0);
+}
 inline int ishmem_team_split_strided(ishmem_team_t parent_team, int start, int stride, int size,
-                                     const void * /*config*/, long /*config_mask*/,
+                                     const ishmem_team_config_t *config, long config_mask,
                                      ishmem_team_t *new_team)
 {
-    return ishmemi_c_team_split_strided(parent_team, start, stride, size, new_team);
+    const int r = ishmemi_c_team_split_strided(parent_team, start, stride, size, new_team);
+    if (r == 0 && new_team && *new_team != ISHMEM_TEAM_INVALID && config && config_mask)
+        return ishmemi_c_team_set_config(*new_team, config_mask, config->num_contexts);
+    return r;
 }
-inline int ishmem_team_split_2d(ishmem_team_t parent_team, int xrange, const void * /*xaxis_config*/,
-                                long /*xaxis_mask*/, ishmem_team_t *xaxis_team,
-                                const void * /*yaxis_config*/, long /*yaxis_mask*/,
+inline int ishmem_team_split_2d(ishmem_team_t parent_team, int xrange, const ishmem_team_config_t *xaxis_config,
+                                long xaxis_mask, ishmem_team_t *xaxis_team,
+                                const ishmem_team_config_t *yaxis_config, long yaxis_mask,
                                 ishmem_team_t *yaxis_team)
 {
-    return ishmemi_c_team_split_2d(parent_team, xrange, xaxis_team, yaxis_team);
+    int r = ishmemi_c_team_split_2d(parent_team, xrange, xaxis_team, yaxis_team);
+    if (r == 0 && xaxis_team && *xaxis_team != ISHMEM_TEAM_INVALID && xaxis_config && xaxis_mask)
+        r = ishmemi_c_team_set_config(*xaxis_team, xaxis_mask, xaxis_config->num_contexts);
+    if (r == 0 && yaxis_team && *yaxis_team != ISHMEM_TEAM_INVALID && yaxis_config && yaxis_mask)
+        r = ishmemi_c_team_set_config(*yaxis_team, yaxis_mask, yaxis_config->num_contexts);
+    return r;
 }
 inline void ishmem_team_destroy(ishmem_team_t team) { ishmemi_c_team_destroy(team); }
 
@@ -258,5 +300,41 @@ inline int ishmem_sum_exscan(T *dest, const T *source, size_t nelems)
 /* fcollect / collect / inscan / exscan typename lists = src/collectives/collect.cpp:44-66,
  * :129-151 and scan.cpp:28-74: the same 23 names as max/min/sum/prod. */
 ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_COLL_TYPED, _, _)
+
+/* ---- broadcast (src/ishmem.h:761-813; the reference's intra-node pull, broadcast_impl.h) ----- */
+inline int ishmem_broadcastmem(ishmem_team_t team, void *dest, const void *source, size_t nbytes, int root)
+{
+    return ishmemi_c_broadcast(team, dest, source, nbytes, root);
+}
+inline int ishmem_broadcastmem(void *dest, const void *source, size_t nbytes, int root)
+{
+    return ishmemi_c_broadcast(ISHMEM_TEAM_WORLD, dest, source, nbytes, root);
+}
+template <typename T>
+inline int ishmem_broadcast(ishmem_team_t team, T *dest, const T *source, size_t nelems, int root)
+{
+    return ishmemi_c_broadcast(team, (void *) dest, (const void *) source, nelems * sizeof(T), root);
+}
+template <typename T>
+inline int ishmem_broadcast(T *dest, const T *source, size_t nelems, int root)
+{
+    return ishmem_broadcast(ISHMEM_TEAM_WORLD, dest, source, nelems, root);
+}
+#define ISHMEMI_CXX_BCAST_TYPED(TYPENAME, TYPE, UNUSED1, UNUSED2)                                   \
+    inline int ishmem_##TYPENAME##_broadcast(ishmem_team_t t, TYPE *d, const TYPE *s, size_t n, int root) \
+    {                                                                                              \
+        return ishmem_broadcast(t, d, s, n, root);                                                 \
+    }                                                                                              \
+    inline int ishmem_##TYPENAME##_broadcast(TYPE *d, const TYPE *s, size_t n, int root)            \
+    {                                                                                              \
+        return ishmem_broadcast(d, s, n, root);                                                    \
+    }
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_BCAST_TYPED, _, _)
+
+/* Compiled as HIP: the device-callable half of this API (the reference's SYCL_EXTERNAL functions:
+ * ishmem_my_pe / ishmem_<TN>_<op>_reduce / ... from inside a kernel, ishmemx_*_work_group). */
+#if defined(__HIP__)
+#include "ishmemx_device.h"
+#endif
 
 #endif /* ISHMEM_AMD_ISHMEM_H */

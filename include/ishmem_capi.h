@@ -58,6 +58,20 @@ typedef enum {
 #define ISHMEMI_C_TEAM_SHARED 1
 #define ISHMEMI_C_TEAM_NODE 2
 
+/* API version and vendor string reported by ishmem_info_get_version / _name (src/ishmem.h:17-21,
+ * src/ishmem.cpp:495-512): the reference API version this library implements. */
+#define ISHMEMI_C_SPEC_MAJOR 1
+#define ISHMEMI_C_SPEC_MINOR 5
+#define ISHMEMI_C_SPEC_PATCH 1
+#define ISHMEMI_C_MAX_NAME_LEN 256
+#define ISHMEMI_C_VENDOR_STRING "ishmem_amd (AMD Instinct MI355X, HIP)"
+
+/* Thread levels (src/ishmem.h:23-26). */
+#define ISHMEMI_C_THREAD_SINGLE 0
+#define ISHMEMI_C_THREAD_FUNNELED 1
+#define ISHMEMI_C_THREAD_SERIALIZED 2
+#define ISHMEMI_C_THREAD_MULTIPLE 3
+
 /* ---- lifecycle — replaces ishmem_init / ishmem_finalize (src/ishmem.h:40-41,
  *      src/ishmem.cpp:224-407) and ishmemx_init_attr (src/ishmemx.h:21-37) ---------------------
  * ishmemi_c_init(): PE identity from the environment: ISHMEM_PE / ISHMEM_NPES, else the
@@ -74,6 +88,12 @@ int ishmemi_c_initialized(void);
 int ishmemi_c_my_pe(void);  /* ishmem_my_pe, src/ishmem.h:54 */
 int ishmemi_c_n_pes(void);  /* ishmem_n_pes, src/ishmem.h:55 */
 int ishmemi_c_device(void); /* HIP device ordinal this PE runs on */
+/* ishmem_init_thread / ishmem_query_thread (src/ishmem.h:44-45, src/ishmem.cpp:409-419): the
+ * runtime's host calls are serialised by one lock, so ISHMEM_THREAD_MULTIPLE is always provided
+ * (collectives of one team must still be called in the same order on every member, as in the
+ * reference, src/teams.h:29-38).  init_thread initialises like ishmemi_c_init. */
+int ishmemi_c_init_thread(int requested, int *provided);
+int ishmemi_c_query_thread(int *provided);
 
 /* ---- symmetric heap in HBM — replaces ishmem_malloc/align/calloc/free (src/ishmem.h:48-51,
  *      src/memory.cpp:200-300) and ishmem_ptr (src/ishmem.h:56) -----------------------------
@@ -95,6 +115,12 @@ int ishmemi_c_team_translate_pe(int src_team, int src_pe, int dest_team);
 int ishmemi_c_team_split_strided(int parent_team, int start, int stride, int size, int *new_team);
 int ishmemi_c_team_split_2d(int parent_team, int xrange, int *xaxis_team, int *yaxis_team);
 void ishmemi_c_team_destroy(int team);
+/* Team configuration (ishmem_team_config_t = {int num_contexts}, src/ishmem.h:63-67, :78;
+ * src/teams.cpp:545-570).  Contexts do not exist on this path; the value given at split time is
+ * stored and reported.  get_config: config_mask 0 or ISHMEM_TEAM_NUM_CONTEXTS (1); returns 0, or
+ * nonzero for an invalid team / mask / a NULL out-pointer with a nonzero mask. */
+int ishmemi_c_team_get_config(int team, long config_mask, int *num_contexts);
+int ishmemi_c_team_set_config(int team, long config_mask, int num_contexts);
 
 /* ---- synchronisation — ishmem_barrier_all / sync_all / team_sync (src/ishmem.h:1555-1559,
  *      device implementation src/collectives/sync_impl.h:30-69) --------------------------------- */
@@ -176,6 +202,10 @@ int ishmemi_c_collect(int team, void *dest, const void *source, size_t nbytes);
 int ishmemi_c_collect_on_stream(int team, void *dest, const void *source, size_t nbytes, int *ret,
                                 void *stream);
 int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *source, size_t nelems);
+/* broadcast: dest on every member (the root included) = the root's `nbytes` of source
+ * (ishmem_<TN>_broadcast / ishmem_broadcastmem, src/ishmem.h:761-813, broadcast_impl.h's pull
+ * variant).  `root` is the root's index in the team.  Sources outside the heap are staged. */
+int ishmemi_c_broadcast(int team, void *dest, const void *source, size_t nbytes, int root);
 int ishmemi_c_scan_on_stream(int team, int dtype, int inclusive, void *dest, const void *source,
                              size_t nelems, int *ret, void *stream);
 /* The `deps` / returned-event plumbing of every _on_queue form (fcollect, collect, inscan, exscan;
@@ -209,6 +239,12 @@ typedef struct {
     uint64_t *dev_counts;                         /* symmetric [team][8] u64: device collect counts */
 } ishmemi_c_device_ctx_t;
 void *ishmemi_c_device_ctx(void);
+/* Device-API context slots: every HIP translation unit that includes ishmemx_device.h owns a
+ * `__device__ const ishmemi_c_device_ctx_t *` and registers the address of its host shadow here
+ * from a static initializer.  init writes the context's device address into every registered slot
+ * (hipMemcpyToSymbol) and finalize clears them; a slot registered after init is written at once.
+ * Returns 0. */
+int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
 
 /* ---- diagnostics / parameters ----------------------------------------------------------------
  * ishmemi_c_set_param names: "max_blocks" (workgroups per collective launch, <= 1024),

@@ -22,8 +22,10 @@
  * no reference counterpart — the reference aborts, src/proxy.cpp:79-84). */
 inline int ishmemx_resync(void) { return ishmemi_c_resync(); }
 
+#ifndef __HIP__
 typedef struct ihipStream_t *hipStream_t; /* identical to HIP's own typedefs */
 typedef struct ihipEvent_t *hipEvent_t;
+#endif
 
 namespace ishmemi_cxx {
 template <typename T>

@@ -239,6 +239,7 @@ template <typename G, typename T, int OP>
 __device__ int reduce_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, const T *source,
                             size_t nreduce)
 {
+    if (!c || team < 0 || team >= ISHMEMI_C_MAX_TEAMS) return 1;  // not initialised / bad handle
     const int tid = G::rank(), nthr = G::size();
     const int size = c->team_size[team], me = c->team_my_idx[team];
     if (size <= 0 || me < 0) return 1;
@@ -389,6 +390,7 @@ template <typename G>
 __device__ inline int collect_group(const ishmemi_c_device_ctx_t *c, int team, void *dest, const void *source,
                                     size_t mybytes, bool equal)
 {
+    if (!c || team < 0 || team >= ISHMEMI_C_MAX_TEAMS) return 1;  // not initialised / bad handle
     const int size = c->team_size[team], me = c->team_my_idx[team];
     if (size <= 0 || me < 0) return 1;
     const uint32_t epoch = group_epoch<G>(c, team);
@@ -421,6 +423,7 @@ template <typename G, typename T>
 __device__ inline int scan_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, const T *source,
                                  size_t nelems, bool inclusive)
 {
+    if (!c || team < 0 || team >= ISHMEMI_C_MAX_TEAMS) return 1;  // not initialised / bad handle
     const int tid = G::rank(), nthr = G::size();
     const int size = c->team_size[team], me = c->team_my_idx[team];
     // dest and source must be disjoint: a peer may still be reading this PE's source.
@@ -520,34 +523,134 @@ constexpr bool is_canon()
 
 }  // namespace ishmemx_dev
 
+/* ---- library queries from a kernel (src/ishmem.h:54-58, :74-77: host and device) ------------ */
+__device__ inline int ishmem_my_pe(void)
+{
+    const ishmemi_c_device_ctx_t *c = ishmemx_dev::ctx();
+    return c ? c->pe : -1;
+}
+__device__ inline int ishmem_n_pes(void)
+{
+    const ishmemi_c_device_ctx_t *c = ishmemx_dev::ctx();
+    return c ? c->npes : -1;
+}
+__device__ inline void *ishmem_ptr(const void *dest, int pe)
+{
+    const ishmemi_c_device_ctx_t *c = ishmemx_dev::ctx();
+    if (!c || pe < 0 || pe >= c->npes) return nullptr;
+    const uint64_t off = (uint64_t) ((const char *) dest - c->heap_base);
+    return off < c->heap_size ? (void *) (c->peer_heap[pe] + off) : nullptr;
+}
+__device__ inline int ishmem_team_my_pe(int team)
+{
+    const ishmemi_c_device_ctx_t *c = ishmemx_dev::ctx();
+    if (!c || team < 0 || team >= ISHMEMI_C_MAX_TEAMS || c->team_size[team] <= 0) return -1;
+    return c->team_my_idx[team];
+}
+__device__ inline int ishmem_team_n_pes(int team)
+{
+    const ishmemi_c_device_ctx_t *c = ishmemx_dev::ctx();
+    if (!c || team < 0 || team >= ISHMEMI_C_MAX_TEAMS || c->team_size[team] <= 0) return -1;
+    return c->team_size[team];
+}
+__device__ inline int ishmem_team_translate_pe(int src_team, int src_pe, int dest_team)
+{
+    const ishmemi_c_device_ctx_t *c = ishmemx_dev::ctx();
+    if (!c || src_team < 0 || src_team >= ISHMEMI_C_MAX_TEAMS || dest_team < 0 ||
+        dest_team >= ISHMEMI_C_MAX_TEAMS || c->team_size[src_team] <= 0 || c->team_size[dest_team] <= 0 ||
+        src_pe < 0 || src_pe >= c->team_size[src_team])
+        return -1;
+    const int d = c->team_start[src_team] + src_pe * c->team_stride[src_team] - c->team_start[dest_team];
+    const int st = c->team_stride[dest_team];
+    if (st == 0 || d % st) return -1;
+    return (d / st >= 0 && d / st < c->team_size[dest_team]) ? d / st : -1;
+}
+__device__ inline void ishmem_info_get_version(int *major, int *minor)
+{
+    *major = ISHMEMI_C_SPEC_MAJOR;
+    *minor = ISHMEMI_C_SPEC_MINOR;
+}
+__device__ inline void ishmem_info_get_name(char *name)
+{
+    const char *v = ISHMEMI_C_VENDOR_STRING;
+    while (*v) *name++ = *v++;
+    *name = '\0';
+}
+
+/* ---- synchronisation from a kernel (src/ishmem.h:1555-1559, src/ishmemx.h:2228-2239) -------- */
+__device__ inline void ishmem_barrier_all(void)
+{
+    (void) ishmemx_dev::team_sync_group<ishmemx_dev::thread_t>(ishmemx_dev::ctx(), ISHMEMI_C_TEAM_WORLD);
+}
+__device__ inline void ishmem_sync_all(void)
+{
+    (void) ishmemx_dev::team_sync_group<ishmemx_dev::thread_t>(ishmemx_dev::ctx(), ISHMEMI_C_TEAM_WORLD);
+}
+__device__ inline int ishmem_team_sync(int team)
+{
+    return ishmemx_dev::team_sync_group<ishmemx_dev::thread_t>(ishmemx_dev::ctx(), team);
+}
+template <typename Group>
+__device__ inline void ishmemx_barrier_all_work_group(const Group &)
+{
+    (void) ishmemx_dev::team_sync_group<ishmemx_dev::exec_t<Group>>(ishmemx_dev::ctx(), ISHMEMI_C_TEAM_WORLD);
+}
+template <typename Group>
+__device__ inline void ishmemx_sync_all_work_group(const Group &)
+{
+    (void) ishmemx_dev::team_sync_group<ishmemx_dev::exec_t<Group>>(ishmemx_dev::ctx(), ISHMEMI_C_TEAM_WORLD);
+}
+template <typename Group>
+__device__ inline void ishmemx_team_sync_work_group(int team, const Group &)
+{
+    (void) ishmemx_dev::team_sync_group<ishmemx_dev::exec_t<Group>>(ishmemx_dev::ctx(), team);
+}
+
+/* ---- device print (src/ishmemx.h:2256-2271; the reference sends it to a host proxy thread, a
+ *      HIP kernel prints directly) --------------------------------------------------------------- */
+typedef enum { DEBUG, WARNING, ERROR, STDOUT, STDERR } ishmemx_print_msg_type_t;
+__device__ inline void ishmemx_print(const char *file, long int line, const char *func, const char *out,
+                                     ishmemx_print_msg_type_t msg_type)
+{
+    const char *kind = msg_type == DEBUG ? "DEBUG" : msg_type == WARNING ? "WARN" : msg_type == ERROR ? "ERROR" : "";
+    if (file) printf("[%d] %s %s:%ld %s: %s", ishmem_my_pe(), kind, file, line, func ? func : "", out);
+    else printf("[%d] %s%s%s", ishmem_my_pe(), kind, *kind ? ": " : "", out);
+}
+__device__ inline void ishmemx_print(const char *out, ishmemx_print_msg_type_t msg_type)
+{
+    ishmemx_print(nullptr, 0, nullptr, out, msg_type);
+}
+__device__ inline void ishmemx_print(const char *out) { ishmemx_print(nullptr, 0, nullptr, out, DEBUG); }
+
+/* ---- reductions ------------------------------------------------------------------------------ */
 #define ISHMEMX_DEV_GENERIC(OPNAME, OPC)                                                           \
-    template <typename T, typename G = ishmemx_dev::work_group_t>                                  \
-    __device__ inline int ishmemx_##OPNAME##_reduce_work_group(                                    \
-        const ishmemi_c_device_ctx_t *ctx, T *dest, const T *source, size_t nreduce, G = G())      \
+    template <typename T, typename Group>                                                          \
+    __device__ inline int ishmemx_##OPNAME##_reduce_work_group(T *dest, const T *source,           \
+                                                               size_t nreduce, const Group &)      \
     {                                                                                              \
-        return ishmemx_dev::reduce_group<G, T, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,       \
-                                                    nreduce);                                      \
+        return ishmemx_dev::reduce_group<ishmemx_dev::exec_t<Group>, T, OPC>(                      \
+            ishmemx_dev::ctx(), ISHMEMI_C_TEAM_WORLD, dest, source, nreduce);                      \
     }                                                                                              \
-    template <typename T, typename G = ishmemx_dev::work_group_t>                                  \
-    __device__ inline int ishmemx_##OPNAME##_reduce_work_group(                                    \
-        const ishmemi_c_device_ctx_t *ctx, int team, T *dest, const T *source, size_t nreduce,     \
-        G = G())                                                                                   \
+    template <typename T, typename Group>                                                          \
+    __device__ inline int ishmemx_##OPNAME##_reduce_work_group(int team, T *dest, const T *source, \
+                                                               size_t nreduce, const Group &)      \
     {                                                                                              \
-        return ishmemx_dev::reduce_group<G, T, OPC>(ctx, team, dest, source, nreduce);             \
+        return ishmemx_dev::reduce_group<ishmemx_dev::exec_t<Group>, T, OPC>(ishmemx_dev::ctx(),   \
+                                                                             team, dest, source,   \
+                                                                             nreduce);             \
     }                                                                                              \
     template <typename T>                                                                          \
-    __device__ inline int ishmem_##OPNAME##_reduce(const ishmemi_c_device_ctx_t *ctx, T *dest,     \
-                                                   const T *source, size_t nreduce)                \
+    __device__ inline int ishmem_##OPNAME##_reduce(T *dest, const T *source, size_t nreduce)       \
     {                                                                                              \
-        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, T, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, \
+        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, T, OPC>(                           \
+            ishmemx_dev::ctx(), ISHMEMI_C_TEAM_WORLD, dest, source, nreduce);                      \
+    }                                                                                              \
+    template <typename T>                                                                          \
+    __device__ inline int ishmem_##OPNAME##_reduce(int team, T *dest, const T *source,             \
+                                                   size_t nreduce)                                 \
+    {                                                                                              \
+        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, T, OPC>(ishmemx_dev::ctx(), team,  \
                                                                         dest, source, nreduce);    \
-    }                                                                                              \
-    template <typename T>                                                                          \
-    __device__ inline int ishmem_##OPNAME##_reduce(const ishmemi_c_device_ctx_t *ctx, int team,    \
-                                                   T *dest, const T *source, size_t nreduce)       \
-    {                                                                                              \
-        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, T, OPC>(ctx, team, dest, source,   \
-                                                                        nreduce);                  \
     }
 
 ISHMEMX_DEV_GENERIC(and, ISHMEMI_OP_AND)
@@ -559,134 +662,213 @@ ISHMEMX_DEV_GENERIC(sum, ISHMEMI_OP_SUM)
 ISHMEMX_DEV_GENERIC(prod, ISHMEMI_OP_PROD)
 
 #define ISHMEMX_DEV_TYPED(TYPENAME, TYPE, OPNAME, OPC)                                              \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
+    template <typename Group>                                                                      \
     __device__ inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_work_group(                       \
-        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nreduce,         \
-        G = G())                                                                                   \
+        TYPE *dest, const TYPE *source, size_t nreduce, const Group &grp)                          \
     {                                                                                              \
-        return ishmemx_dev::reduce_group<G, TYPE, OPC>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,    \
-                                                       nreduce);                                   \
+        return ishmemx_##OPNAME##_reduce_work_group<TYPE>(dest, source, nreduce, grp);             \
     }                                                                                              \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
+    template <typename Group>                                                                      \
     __device__ inline int ishmemx_##TYPENAME##_##OPNAME##_reduce_work_group(                       \
-        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source,               \
-        size_t nreduce, G = G())                                                                   \
+        int team, TYPE *dest, const TYPE *source, size_t nreduce, const Group &grp)                \
     {                                                                                              \
-        return ishmemx_dev::reduce_group<G, TYPE, OPC>(ctx, team, dest, source, nreduce);          \
+        return ishmemx_##OPNAME##_reduce_work_group<TYPE>(team, dest, source, nreduce, grp);       \
     }                                                                                              \
-    __device__ inline int ishmem_##TYPENAME##_##OPNAME##_reduce(                                   \
-        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nreduce)         \
+    __device__ inline int ishmem_##TYPENAME##_##OPNAME##_reduce(TYPE *dest, const TYPE *source,    \
+                                                                size_t nreduce)                    \
     {                                                                                              \
-        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, TYPE, OPC>(                        \
-            ctx, ISHMEMI_C_TEAM_WORLD, dest, source, nreduce);                                     \
+        return ishmem_##OPNAME##_reduce<TYPE>(dest, source, nreduce);                              \
     }                                                                                              \
-    __device__ inline int ishmem_##TYPENAME##_##OPNAME##_reduce(                                   \
-        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source,               \
-        size_t nreduce)                                                                            \
+    __device__ inline int ishmem_##TYPENAME##_##OPNAME##_reduce(int team, TYPE *dest,              \
+                                                                const TYPE *source, size_t nreduce) \
     {                                                                                              \
-        return ishmemx_dev::reduce_group<ishmemx_dev::thread_t, TYPE, OPC>(ctx, team, dest,        \
-                                                                           source, nreduce);       \
+        return ishmem_##OPNAME##_reduce<TYPE>(team, dest, source, nreduce);                        \
     }
 
-/* fcollect / collect / sum_inscan / sum_exscan: work-group (or wavefront) and one-work-item forms
- * for the reference's 23 arithmetic typenames, plus fcollectmem / collectmem. */
-#define ISHMEMX_DEV_COLL(TYPENAME, TYPE, UNUSED1, UNUSED2)                                          \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
-    __device__ inline int ishmemx_##TYPENAME##_fcollect_work_group(                                \
-        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source, size_t nelems, \
-        G = G())                                                                                   \
-    {                                                                                              \
-        return ishmemx_dev::collect_group<G>(ctx, team, dest, source, nelems * sizeof(TYPE), true); \
-    }                                                                                              \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
-    __device__ inline int ishmemx_##TYPENAME##_fcollect_work_group(                                \
-        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nelems, G = G())  \
-    {                                                                                              \
-        return ishmemx_##TYPENAME##_fcollect_work_group<G>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source, \
-                                                           nelems);                                \
-    }                                                                                              \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
-    __device__ inline int ishmemx_##TYPENAME##_collect_work_group(                                 \
-        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source, size_t nelems, \
-        G = G())                                                                                   \
-    {                                                                                              \
-        return ishmemx_dev::collect_group<G>(ctx, team, dest, source, nelems * sizeof(TYPE), false); \
-    }                                                                                              \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
-    __device__ inline int ishmemx_##TYPENAME##_collect_work_group(                                 \
-        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nelems, G = G())  \
-    {                                                                                              \
-        return ishmemx_##TYPENAME##_collect_work_group<G>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source,  \
-                                                          nelems);                                 \
-    }                                                                                              \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
-    __device__ inline int ishmemx_##TYPENAME##_sum_inscan_work_group(                              \
-        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source, size_t nelems, \
-        G = G())                                                                                   \
-    {                                                                                              \
-        return ishmemx_dev::scan_group<G, TYPE>(ctx, team, dest, source, nelems, true);            \
-    }                                                                                              \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
-    __device__ inline int ishmemx_##TYPENAME##_sum_inscan_work_group(                              \
-        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nelems, G = G())  \
-    {                                                                                              \
-        return ishmemx_dev::scan_group<G, TYPE>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source, nelems,   \
-                                                true);                                             \
-    }                                                                                              \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
-    __device__ inline int ishmemx_##TYPENAME##_sum_exscan_work_group(                              \
-        const ishmemi_c_device_ctx_t *ctx, int team, TYPE *dest, const TYPE *source, size_t nelems, \
-        G = G())                                                                                   \
-    {                                                                                              \
-        return ishmemx_dev::scan_group<G, TYPE>(ctx, team, dest, source, nelems, false);           \
-    }                                                                                              \
-    template <typename G = ishmemx_dev::work_group_t>                                              \
-    __device__ inline int ishmemx_##TYPENAME##_sum_exscan_work_group(                              \
-        const ishmemi_c_device_ctx_t *ctx, TYPE *dest, const TYPE *source, size_t nelems, G = G())  \
-    {                                                                                              \
-        return ishmemx_dev::scan_group<G, TYPE>(ctx, ISHMEMI_C_TEAM_WORLD, dest, source, nelems,   \
-                                                false);                                            \
-    }                                                                                              \
-    __device__ inline int ishmem_##TYPENAME##_fcollect(const ishmemi_c_device_ctx_t *ctx, int team, \
-                                                       TYPE *dest, const TYPE *source,             \
-                                                       size_t nelems)                              \
-    {                                                                                              \
-        return ishmemx_dev::collect_group<ishmemx_dev::thread_t>(ctx, team, dest, source,          \
-                                                                 nelems * sizeof(TYPE), true);     \
-    }                                                                                              \
-    __device__ inline int ishmem_##TYPENAME##_collect(const ishmemi_c_device_ctx_t *ctx, int team, \
-                                                      TYPE *dest, const TYPE *source,              \
-                                                      size_t nelems)                               \
-    {                                                                                              \
-        return ishmemx_dev::collect_group<ishmemx_dev::thread_t>(ctx, team, dest, source,          \
-                                                                 nelems * sizeof(TYPE), false);    \
-    }                                                                                              \
-    __device__ inline int ishmem_##TYPENAME##_sum_inscan(const ishmemi_c_device_ctx_t *ctx,        \
-                                                         int team, TYPE *dest, const TYPE *source, \
-                                                         size_t nelems)                            \
-    {                                                                                              \
-        return ishmemx_dev::scan_group<ishmemx_dev::thread_t, TYPE>(ctx, team, dest, source,       \
-                                                                    nelems, true);                 \
-    }                                                                                              \
-    __device__ inline int ishmem_##TYPENAME##_sum_exscan(const ishmemi_c_device_ctx_t *ctx,        \
-                                                         int team, TYPE *dest, const TYPE *source, \
-                                                         size_t nelems)                            \
-    {                                                                                              \
-        return ishmemx_dev::scan_group<ishmemx_dev::thread_t, TYPE>(ctx, team, dest, source,       \
-                                                                    nelems, false);                \
-    }
-
-template <typename G = ishmemx_dev::work_group_t>
-__device__ inline int ishmemx_fcollectmem_work_group(const ishmemi_c_device_ctx_t *ctx, int team, void *dest,
-                                                     const void *source, size_t nbytes, G = G())
+/* ---- fcollect / collect / sum_inscan / sum_exscan / broadcast --------------------------------- */
+template <typename T, typename Group>
+__device__ inline int ishmemx_fcollect_work_group(int team, T *dest, const T *source, size_t nelems, const Group &)
 {
-    return ishmemx_dev::collect_group<G>(ctx, team, dest, source, nbytes, true);
+    return ishmemx_dev::collect_group<ishmemx_dev::exec_t<Group>>(ishmemx_dev::ctx(), team, dest, source,
+                                                                  nelems * sizeof(T), true);
 }
-template <typename G = ishmemx_dev::work_group_t>
-__device__ inline int ishmemx_collectmem_work_group(const ishmemi_c_device_ctx_t *ctx, int team, void *dest,
-                                                    const void *source, size_t nbytes, G = G())
+template <typename T, typename Group>
+__device__ inline int ishmemx_collect_work_group(int team, T *dest, const T *source, size_t nelems, const Group &)
 {
-    return ishmemx_dev::collect_group<G>(ctx, team, dest, source, nbytes, false);
+    return ishmemx_dev::collect_group<ishmemx_dev::exec_t<Group>>(ishmemx_dev::ctx(), team, dest, source,
+                                                                  nelems * sizeof(T), false);
+}
+template <typename T, typename Group>
+__device__ inline int ishmemx_sum_inscan_work_group(int team, T *dest, const T *source, size_t nelems, const Group &)
+{
+    return ishmemx_dev::scan_group<ishmemx_dev::exec_t<Group>, T>(ishmemx_dev::ctx(), team, dest, source, nelems,
+                                                                  true);
+}
+template <typename T, typename Group>
+__device__ inline int ishmemx_sum_exscan_work_group(int team, T *dest, const T *source, size_t nelems, const Group &)
+{
+    return ishmemx_dev::scan_group<ishmemx_dev::exec_t<Group>, T>(ishmemx_dev::ctx(), team, dest, source, nelems,
+                                                                  false);
+}
+template <typename T, typename Group>
+__device__ inline int ishmemx_broadcast_work_group(int team, T *dest, const T *source, size_t nelems, int root,
+                                                   const Group &)
+{
+    return ishmemx_dev::broadcast_group<ishmemx_dev::exec_t<Group>>(ishmemx_dev::ctx(), team, dest, source,
+                                                                    nelems * sizeof(T), root);
+}
+#define ISHMEMX_DEV_COLL_WORLD(NAME)                                                                \
+    template <typename T, typename Group>                                                          \
+    __device__ inline int ishmemx_##NAME##_work_group(T *dest, const T *source, size_t nelems,      \
+                                                      const Group &grp)                            \
+    {                                                                                              \
+        return ishmemx_##NAME##_work_group<T>(ISHMEMI_C_TEAM_WORLD, dest, source, nelems, grp);    \
+    }                                                                                              \
+    template <typename T>                                                                          \
+    __device__ inline int ishmem_##NAME(int team, T *dest, const T *source, size_t nelems)         \
+    {                                                                                              \
+        return ishmemx_##NAME##_work_group<T>(team, dest, source, nelems, ishmemx_dev::thread);    \
+    }                                                                                              \
+    template <typename T>                                                                          \
+    __device__ inline int ishmem_##NAME(T *dest, const T *source, size_t nelems)                   \
+    {                                                                                              \
+        return ishmemx_##NAME##_work_group<T>(ISHMEMI_C_TEAM_WORLD, dest, source, nelems,          \
+                                              ishmemx_dev::thread);                                \
+    }
+ISHMEMX_DEV_COLL_WORLD(fcollect)
+ISHMEMX_DEV_COLL_WORLD(collect)
+ISHMEMX_DEV_COLL_WORLD(sum_inscan)
+ISHMEMX_DEV_COLL_WORLD(sum_exscan)
+template <typename T, typename Group>
+__device__ inline int ishmemx_broadcast_work_group(T *dest, const T *source, size_t nelems, int root, const Group &grp)
+{
+    return ishmemx_broadcast_work_group<T>(ISHMEMI_C_TEAM_WORLD, dest, source, nelems, root, grp);
+}
+template <typename T>
+__device__ inline int ishmem_broadcast(int team, T *dest, const T *source, size_t nelems, int root)
+{
+    return ishmemx_broadcast_work_group<T>(team, dest, source, nelems, root, ishmemx_dev::thread);
+}
+template <typename T>
+__device__ inline int ishmem_broadcast(T *dest, const T *source, size_t nelems, int root)
+{
+    return ishmemx_broadcast_work_group<T>(ISHMEMI_C_TEAM_WORLD, dest, source, nelems, root, ishmemx_dev::thread);
+}
+
+/* Typed forms for the reference's 23 arithmetic typenames (collect.cpp:44-66, :129-151,
+ * scan.cpp:28-74, broadcast.cpp): work-group and one-work-item, with and without a team. */
+#define ISHMEMX_DEV_COLL_TYPED_ONE(TYPENAME, TYPE, NAME)                                             \
+    template <typename Group>                                                                      \
+    __device__ inline int ishmemx_##TYPENAME##_##NAME##_work_group(int team, TYPE *dest,            \
+                                                                   const TYPE *source,              \
+                                                                   size_t nelems, const Group &grp) \
+    {                                                                                              \
+        return ishmemx_##NAME##_work_group<TYPE>(team, dest, source, nelems, grp);                 \
+    }                                                                                              \
+    template <typename Group>                                                                      \
+    __device__ inline int ishmemx_##TYPENAME##_##NAME##_work_group(TYPE *dest, const TYPE *source,  \
+                                                                   size_t nelems, const Group &grp) \
+    {                                                                                              \
+        return ishmemx_##NAME##_work_group<TYPE>(dest, source, nelems, grp);                       \
+    }                                                                                              \
+    __device__ inline int ishmem_##TYPENAME##_##NAME(int team, TYPE *dest, const TYPE *source,      \
+                                                     size_t nelems)                                \
+    {                                                                                              \
+        return ishmem_##NAME<TYPE>(team, dest, source, nelems);                                    \
+    }                                                                                              \
+    __device__ inline int ishmem_##TYPENAME##_##NAME(TYPE *dest, const TYPE *source, size_t nelems) \
+    {                                                                                              \
+        return ishmem_##NAME<TYPE>(dest, source, nelems);                                          \
+    }
+#define ISHMEMX_DEV_COLL(TYPENAME, TYPE, UNUSED1, UNUSED2)                                          \
+    ISHMEMX_DEV_COLL_TYPED_ONE(TYPENAME, TYPE, fcollect)                                            \
+    ISHMEMX_DEV_COLL_TYPED_ONE(TYPENAME, TYPE, collect)                                             \
+    ISHMEMX_DEV_COLL_TYPED_ONE(TYPENAME, TYPE, sum_inscan)                                          \
+    ISHMEMX_DEV_COLL_TYPED_ONE(TYPENAME, TYPE, sum_exscan)                                          \
+    template <typename Group>                                                                      \
+    __device__ inline int ishmemx_##TYPENAME##_broadcast_work_group(                               \
+        int team, TYPE *dest, const TYPE *source, size_t nelems, int root, const Group &grp)       \
+    {                                                                                              \
+        return ishmemx_broadcast_work_group<TYPE>(team, dest, source, nelems, root, grp);          \
+    }                                                                                              \
+    template <typename Group>                                                                      \
+    __device__ inline int ishmemx_##TYPENAME##_broadcast_work_group(                               \
+        TYPE *dest, const TYPE *source, size_t nelems, int root, const Group &grp)                 \
+    {                                                                                              \
+        return ishmemx_broadcast_work_group<TYPE>(dest, source, nelems, root, grp);                \
+    }                                                                                              \
+    __device__ inline int ishmem_##TYPENAME##_broadcast(int team, TYPE *dest, const TYPE *source,   \
+                                                        size_t nelems, int root)                   \
+    {                                                                                              \
+        return ishmem_broadcast<TYPE>(team, dest, source, nelems, root);                           \
+    }                                                                                              \
+    __device__ inline int ishmem_##TYPENAME##_broadcast(TYPE *dest, const TYPE *source,             \
+                                                        size_t nelems, int root)                   \
+    {                                                                                              \
+        return ishmem_broadcast<TYPE>(dest, source, nelems, root);                                 \
+    }
+
+/* byte forms: fcollectmem / collectmem / broadcastmem */
+template <typename Group>
+__device__ inline int ishmemx_fcollectmem_work_group(int team, void *dest, const void *source, size_t nbytes,
+                                                     const Group &)
+{
+    return ishmemx_dev::collect_group<ishmemx_dev::exec_t<Group>>(ishmemx_dev::ctx(), team, dest, source, nbytes,
+                                                                  true);
+}
+template <typename Group>
+__device__ inline int ishmemx_fcollectmem_work_group(void *dest, const void *source, size_t nbytes, const Group &grp)
+{
+    return ishmemx_fcollectmem_work_group(ISHMEMI_C_TEAM_WORLD, dest, source, nbytes, grp);
+}
+template <typename Group>
+__device__ inline int ishmemx_collectmem_work_group(int team, void *dest, const void *source, size_t nbytes,
+                                                    const Group &)
+{
+    return ishmemx_dev::collect_group<ishmemx_dev::exec_t<Group>>(ishmemx_dev::ctx(), team, dest, source, nbytes,
+                                                                  false);
+}
+template <typename Group>
+__device__ inline int ishmemx_collectmem_work_group(void *dest, const void *source, size_t nbytes, const Group &grp)
+{
+    return ishmemx_collectmem_work_group(ISHMEMI_C_TEAM_WORLD, dest, source, nbytes, grp);
+}
+template <typename Group>
+__device__ inline int ishmemx_broadcastmem_work_group(int team, void *dest, const void *source, size_t nbytes,
+                                                      int root, const Group &)
+{
+    return ishmemx_dev::broadcast_group<ishmemx_dev::exec_t<Group>>(ishmemx_dev::ctx(), team, dest, source, nbytes,
+                                                                    root);
+}
+template <typename Group>
+__device__ inline int ishmemx_broadcastmem_work_group(void *dest, const void *source, size_t nbytes, int root,
+                                                      const Group &grp)
+{
+    return ishmemx_broadcastmem_work_group(ISHMEMI_C_TEAM_WORLD, dest, source, nbytes, root, grp);
+}
+__device__ inline int ishmem_fcollectmem(int team, void *dest, const void *source, size_t nbytes)
+{
+    return ishmemx_fcollectmem_work_group(team, dest, source, nbytes, ishmemx_dev::thread);
+}
+__device__ inline int ishmem_fcollectmem(void *dest, const void *source, size_t nbytes)
+{
+    return ishmemx_fcollectmem_work_group(ISHMEMI_C_TEAM_WORLD, dest, source, nbytes, ishmemx_dev::thread);
+}
+__device__ inline int ishmem_collectmem(int team, void *dest, const void *source, size_t nbytes)
+{
+    return ishmemx_collectmem_work_group(team, dest, source, nbytes, ishmemx_dev::thread);
+}
+__device__ inline int ishmem_collectmem(void *dest, const void *source, size_t nbytes)
+{
+    return ishmemx_collectmem_work_group(ISHMEMI_C_TEAM_WORLD, dest, source, nbytes, ishmemx_dev::thread);
+}
+__device__ inline int ishmem_broadcastmem(int team, void *dest, const void *source, size_t nbytes, int root)
+{
+    return ishmemx_broadcastmem_work_group(team, dest, source, nbytes, root, ishmemx_dev::thread);
+}
+__device__ inline int ishmem_broadcastmem(void *dest, const void *source, size_t nbytes, int root)
+{
+    return ishmemx_broadcastmem_work_group(ISHMEMI_C_TEAM_WORLD, dest, source, nbytes, root, ishmemx_dev::thread);
 }
 
 /* Same TYPENAME x op matrix as the host API (src/collectives/reduce.cpp:95-417). */

@@ -72,6 +72,35 @@ def init(pe: int = 0, npes: int = 1, device: int = -1, key: str | None = None) -
         raise RuntimeError(f"ishmem init failed: {last_error()}")
 
 
+def ishmem_init_thread(requested: int) -> tuple[int, int]:
+    """ishmem_init_thread (src/ishmem.h:44): returns (status, provided); always
+    ISHMEM_THREAD_MULTIPLE (src/ishmem.cpp:409-419)."""
+    prov = ctypes.c_int(-1)
+    r = _L.ishmemi_c_init_thread(requested, ctypes.byref(prov))
+    return r, prov.value
+
+
+def ishmem_query_thread() -> int:
+    prov = ctypes.c_int(-1)
+    _L.ishmemi_c_query_thread(ctypes.byref(prov))
+    return prov.value
+
+
+ISHMEM_THREAD_SINGLE, ISHMEM_THREAD_FUNNELED, ISHMEM_THREAD_SERIALIZED, ISHMEM_THREAD_MULTIPLE = 0, 1, 2, 3
+ISHMEM_MAJOR_VERSION, ISHMEM_MINOR_VERSION = 1, 5
+ISHMEM_VENDOR_STRING = "ishmem_amd (AMD Instinct MI355X, HIP)"
+ISHMEM_TEAM_NUM_CONTEXTS = 1
+
+
+def ishmem_info_get_version() -> tuple[int, int]:
+    """(major, minor) of the reference API implemented (src/ishmem.h:17-18, :57)."""
+    return ISHMEM_MAJOR_VERSION, ISHMEM_MINOR_VERSION
+
+
+def ishmem_info_get_name() -> str:
+    return ISHMEM_VENDOR_STRING
+
+
 def ishmem_finalize() -> None:
     _L.ishmemi_c_finalize()
 
@@ -150,6 +179,13 @@ def ishmem_team_split_2d(parent: int, xrange: int) -> tuple[int, int, int]:
 
 def ishmem_team_destroy(team: int) -> None:
     _L.ishmemi_c_team_destroy(team)
+
+
+def ishmem_team_get_config(team: int, config_mask: int = ISHMEM_TEAM_NUM_CONTEXTS) -> tuple[int, int]:
+    """(status, num_contexts) (src/ishmem.h:78, src/teams.cpp:545-570)."""
+    n = ctypes.c_int(0)
+    r = _L.ishmemi_c_team_get_config(team, config_mask, ctypes.byref(n))
+    return r, n.value
 
 
 def ishmem_barrier_all() -> int:
@@ -277,6 +313,12 @@ def fcollect_on_stream(dest: int, source: int, nbytes: int, ret: int | None, str
     return _L.ishmemi_c_fcollect_on_stream(team, dest, source, nbytes, ret or None, stream or None)
 
 
+def ishmem_broadcastmem(*args) -> int:
+    """ishmem_broadcastmem([team,] dest, source, nbytes, root) -> int (src/ishmem.h:786, :813)."""
+    team, (dest, source, n, root) = (ISHMEM_TEAM_WORLD, args) if len(args) == 4 else (args[0], args[1:])
+    return _L.ishmemi_c_broadcast(team, dest, source, n, root)
+
+
 def scan(dtype: str, inclusive: bool, dest: int, source: int, nelems: int,
          team: int = ISHMEM_TEAM_WORLD) -> int:
     return _L.ishmemi_c_scan(team, DTYPES[dtype], 1 if inclusive else 0, dest, source, nelems)
@@ -284,6 +326,9 @@ def scan(dtype: str, inclusive: bool, dest: int, source: int, nelems: int,
 
 def _make_coll(kind: str, dt: str, size: int):
     def fn(*args):
+        if kind == "broadcast":  # ([team,] dest, source, nelems, root)
+            team, (dest, source, n, root) = (ISHMEM_TEAM_WORLD, args) if len(args) == 4 else (args[0], args[1:])
+            return _L.ishmemi_c_broadcast(team, dest, source, n * size, root)
         team, (dest, source, n) = (ISHMEM_TEAM_WORLD, args) if len(args) == 3 else (args[0], args[1:])
         if kind == "fcollect":
             return _L.ishmemi_c_fcollect(team, dest, source, n * size)
@@ -299,7 +344,8 @@ _SIZES = {"int8": 1, "uint8": 1, "int16": 2, "uint16": 2, "int32": 4, "uint32": 
 _mod = sys.modules[__name__]
 for _tn in ARITH_TYPENAMES:  # the reference's fcollect / collect / scan lists = these 23 names
     for _kind, _name in (("fcollect", f"ishmem_{_tn}_fcollect"), ("collect", f"ishmem_{_tn}_collect"),
-                         ("inscan", f"ishmem_{_tn}_sum_inscan"), ("exscan", f"ishmem_{_tn}_sum_exscan")):
+                         ("inscan", f"ishmem_{_tn}_sum_inscan"), ("exscan", f"ishmem_{_tn}_sum_exscan"),
+                         ("broadcast", f"ishmem_{_tn}_broadcast")):
         _f = _make_coll(_kind, TYPENAMES[_tn], _SIZES[TYPENAMES[_tn]])
         _f.__name__ = _name
         setattr(_mod, _name, _f)

@@ -20,6 +20,8 @@ PROTOTYPES = [
     ("ishmemi_c_my_pe", _i, []),
     ("ishmemi_c_n_pes", _i, []),
     ("ishmemi_c_device", _i, []),
+    ("ishmemi_c_init_thread", _i, [_i, ctypes.POINTER(_i)]),
+    ("ishmemi_c_query_thread", _i, [ctypes.POINTER(_i)]),
     ("ishmemi_c_malloc", _vp, [_sz]),
     ("ishmemi_c_align", _vp, [_sz, _sz]),
     ("ishmemi_c_calloc", _vp, [_sz, _sz]),
@@ -32,6 +34,8 @@ PROTOTYPES = [
     ("ishmemi_c_team_split_strided", _i, [_i, _i, _i, _i, ctypes.POINTER(_i)]),
     ("ishmemi_c_team_split_2d", _i, [_i, _i, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     ("ishmemi_c_team_destroy", None, [_i]),
+    ("ishmemi_c_team_get_config", _i, [_i, ctypes.c_long, ctypes.POINTER(_i)]),
+    ("ishmemi_c_team_set_config", _i, [_i, ctypes.c_long, _i]),
     ("ishmemi_c_barrier_all", _i, []),
     ("ishmemi_c_sync_all", _i, []),
     ("ishmemi_c_team_sync", _i, [_i]),
@@ -51,7 +55,9 @@ PROTOTYPES = [
     ("ishmemi_c_collect", _i, [_i, _vp, _vp, _sz]),
     ("ishmemi_c_scan", _i, [_i, _i, _i, _vp, _vp, _sz]),
     ("ishmemi_c_scan_on_stream", _i, [_i, _i, _i, _vp, _vp, _sz, _vp, _vp]),
+    ("ishmemi_c_broadcast", _i, [_i, _vp, _vp, _sz, _i]),
     ("ishmemi_c_device_ctx", _vp, []),
+    ("ishmemi_c_register_device_ctx_slot", _i, [_vp]),
     ("ishmemi_c_last_error", ctypes.c_char_p, []),
     ("ishmemi_c_set_param", _i, [ctypes.c_char_p, _ll]),
     ("ishmemi_c_get_param", _ll, [ctypes.c_char_p]),

@@ -84,10 +84,12 @@ struct Team {
     bool valid = false;
     int start = 0, stride = 1, size = 1;  // in world PEs (src/teams.h:56-76)
     int my_idx = -1;                      // my index in the team, -1 if not a member
+    int num_contexts = 0;                 // ishmem_team_config_t given at split (reported only)
 };
 
 struct PeRecord {
     int32_t pe, pid, device, flags_kind;
+    int32_t flags_kind_requested;  // ISHMEM_FLAGS_KIND (tests): where this PE's ladder started
     char pci_bus[32];  // identifies the physical GPU across processes
     uint64_t heap_size;
     // Launch-shape parameters: the multi-PE kernels pair workgroup b with workgroup b of every
@@ -153,6 +155,33 @@ State &S()
 {
     static State s;
     return s;
+}
+
+// Device-API context slots (ishmemi_c_register_device_ctx_slot): host shadows of the per-code-object
+// `__device__` context pointers of include/ishmemx_device.h.
+struct CtxSlots {
+    std::mutex mu;
+    std::vector<const void *> shadows;
+};
+CtxSlots &ctx_slots()
+{
+    static CtxSlots c;
+    return c;
+}
+
+// Writes `ctx` (device address, or null) into one slot.  A code object whose kernels never use
+// the device API may have dropped the variable: that slot is skipped.
+void write_ctx_slot(const void *shadow, const void *ctx)
+{
+    if (hipMemcpyToSymbol(shadow, &ctx, sizeof(ctx), 0, hipMemcpyHostToDevice) != hipSuccess)
+        (void) hipGetLastError();
+}
+
+void write_ctx_slots(const void *ctx)
+{
+    CtxSlots &c = ctx_slots();
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (const void *sh : c.shadows) write_ctx_slot(sh, ctx);
 }
 
 bool in_heap(const State &s, const void *p)
@@ -566,7 +595,7 @@ int fill_team_sync_args(State &s, int team, A &a, std::string &why)
 
 // nbytes[j] = bytes member j contributes; dest slot of j starts at the sum of the earlier ones.
 int collect_launch(State &s, int team, void *dst, const void *src, const uint64_t *nbytes, int *ret,
-                   hipStream_t st, const uint64_t *dst_off = nullptr)
+                   hipStream_t st, const uint64_t *dst_off = nullptr, const char *const *srcs = nullptr)
 {
     Team &t = s.teams[team];
     if (order_stream(s, st)) return 1;
@@ -577,11 +606,11 @@ int collect_launch(State &s, int team, void *dst, const void *src, const uint64_
     uint64_t off = 0, orv = (uintptr_t) src | (uintptr_t) dst, maxb = 0;
     for (int j = 0; j < t.size; ++j) {
         const int gpe = t.start + j * t.stride;
-        a.src[j] = translate(s, src, gpe);
+        a.src[j] = srcs ? srcs[j] : translate(s, src, gpe);
         if (!a.src[j]) return fail("collect: source must be symmetric-heap memory");
         a.dst_off[j] = dst_off ? dst_off[j] : off;
         a.nbytes[j] = nbytes[j];
-        orv |= a.dst_off[j] | nbytes[j];
+        orv |= a.dst_off[j] | nbytes[j] | (uintptr_t) a.src[j];
         off += nbytes[j];
         maxb = std::max(maxb, nbytes[j]);
     }
@@ -684,8 +713,11 @@ int collect_on_stream_impl(int team, void *dst, const void *src, size_t nbytes, 
     return mark_stream(s, st);
 }
 
+// staged: 1 / 0 = the members agreed (blocking calls exchange it first, see ishmemi_c_fcollect);
+// -1 = this PE decides from its own source (stream-ordered calls: every member must then pass
+// the same kind of source, as their launches must match).
 int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret, hipStream_t st,
-                  bool blocking)
+                  bool blocking, int staged = -1)
 {
     State &s = S();
     std::lock_guard<std::mutex> lk(s.mu);
@@ -700,11 +732,12 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
         if (!device_writable(s, dst)) return fail("fcollect: dest must be heap, device or pinned host memory");
         uint64_t nb[kMaxPes];
         for (int j = 0; j < t.size; ++j) nb[j] = nbytes;
-        // A source outside the heap is staged (every member must pass the same kind of source:
-        // the staged call is several launches).  Zero bytes: only the team synchronises.
+        // A source outside the heap is staged (the staged call is several launches, so the members
+        // must agree on it).  Zero bytes: only the team synchronises.
+        if (staged < 0) staged = in_heap(s, src) ? 0 : 1;
         if (nbytes == 0) {
             if (team_sync_locked(s, team, st, ret)) return 1;
-        } else if (!in_heap(s, src)) {
+        } else if (staged) {
             if (order_stream(s, st) || collect_staged(s, team, (char *) dst, (const char *) src, nb, ret, st)) return 1;
         } else if (collect_launch(s, team, dst, src, nb, ret, st)) {
             return 1;
@@ -716,6 +749,28 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
         if (check_team_errors(s, team)) return 1;
     }
     return 0;
+}
+
+// One u64 per member, in team order, on every member (an 8-byte fcollect through the team
+// scratch): blocking calls agree on their path and on local argument failures with it before
+// anything that must match across members is launched (a member that failed alone would leave
+// its peers waiting for launches that never come).  Called without the state lock.
+constexpr uint64_t kAgreeStaged = 1ull << 62, kAgreeFail = 1ull << 63;
+int team_exchange(int team, uint64_t mine, uint64_t *all)
+{
+    State &s = S();
+    const int p = s.teams[team].size;
+    if (hipMemcpy(s.team_scratch, &mine, 8, hipMemcpyHostToDevice) != hipSuccess)
+        return fail("team exchange: copy failed");
+    if (fcollect_impl(team, s.team_scratch + 64, s.team_scratch, 8, nullptr, 0, true, 0)) return 1;
+    if (hipMemcpy(all, s.team_scratch + 64, 8 * (size_t) p, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail("team exchange: copy failed");
+    return 0;
+}
+
+bool member_call(const State &s, int team)
+{
+    return s.initialized && team >= 0 && team < kMaxTeams && s.teams[team].valid && s.teams[team].my_idx >= 0;
 }
 
 int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_t n, int *ret,
@@ -889,6 +944,9 @@ const char *flag_kind_name(int k)
 int alloc_flags(State &s, int kind, bool exportable, hipIpcMemHandle_t *h)
 {
     const size_t bytes = kFlagAllocBytes;
+    // Test hook: behave as if uncached / fine-grained VRAM could not be allocated (the refusal of
+    // coarse-grained flags across devices is tested with it on a one-GPU box).
+    if (env_ll("ISHMEM_TEST_FLAGS_UNAVAILABLE", 0) != 0) kind = kFlagsCoarse;
     for (int k = kind; k < kFlagKinds; ++k) {
         uint32_t *f = nullptr;
         hipError_t e = k == kFlagsUncached ? hipExtMallocWithFlags((void **) &f, bytes, hipDeviceMallocUncached)
@@ -983,6 +1041,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.pid = (int32_t) getpid();
         mine.device = s.device;
         mine.flags_kind = s.flags_kind;
+        mine.flags_kind_requested = first_kind;
         mine.heap_size = s.heap_size;
         mine.max_blocks = s.max_blocks;
         mine.ll_max_bytes = s.ll_max_bytes;
@@ -992,6 +1051,10 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             (void) hipGetLastError();
             snprintf(mine.pci_bus, sizeof(mine.pci_bus), "dev%d", s.device);
         }
+        // Test hook: a device identity of the test's choosing (PEs sharing the box's one GPU then
+        // count as PEs on different devices wherever the runtime decides by device identity).
+        if (const char *fake = getenv("ISHMEM_TEST_PCI_BUS"))
+            snprintf(mine.pci_bus, sizeof(mine.pci_bus), "%s", fake);
         HIP_TRY(hipIpcGetMemHandle(&mine.heap_handle, s.heap));
         mine.flags_handle = flags_handle;
         PeRecord all[kMaxPes];
@@ -1007,6 +1070,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         int share = 0;
         for (int j = 0; j < npes; ++j)
             share += strncmp(all[j].pci_bus, mine.pci_bus, sizeof(mine.pci_bus)) == 0;
+        bool coarse_forced = false;  // a test asked for coarse-grained flags (ISHMEM_FLAGS_KIND=2)
+        for (int j = 0; j < npes; ++j) coarse_forced = coarse_forced || all[j].flags_kind_requested == kFlagsCoarse;
         set_device_share(share);
         for (int j = 0; j < npes; ++j) {
             if (j == pe) continue;
@@ -1078,11 +1143,20 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             if (++kind >= kFlagKinds) return fail("init: no flag-block memory kind can be imported by every PE");
             fresh = true;
         }
-        if (s.flags_kind == kFlagsCoarse && share < npes)
-            fprintf(stderr,
-                    "ishmem_amd: PE %d: flag block is coarse-grained device memory while PEs span "
-                    "several devices; peers' flag stores may stay invisible to this device's polls "
-                    "(device timeouts). Uncached / fine-grained VRAM could not be shared.\n", pe);
+        if (s.flags_kind == kFlagsCoarse && share < npes && !coarse_forced) {
+            // A line of local coarse-grained memory may stay in this device's L2 while a peer on
+            // another device stores into HBM behind it: the polls could miss the flags and every
+            // collective would end in device timeouts.  Refuse, on every PE alike (the kind,
+            // the device identities and the requests were all agreed / allgathered above).
+            std::string kinds;
+            for (int j = 0; j < npes; ++j)
+                kinds += (j ? ", " : "") + std::string("PE ") + std::to_string(j) + " " +
+                         flag_kind_name(all[j].flags_kind) + " on " + all[j].pci_bus;
+            return fail("init: the PEs span several devices but could only share coarse-grained flag "
+                        "memory (uncached / fine-grained VRAM could not be allocated, exported or imported "
+                        "by every PE: " + kinds + "); peers' flag stores could stay invisible to this "
+                        "device's polls.  ISHMEM_FLAGS_KIND=2 forces it anyway (tests only)");
+        }
         if (s.boot.barrier(err)) return fail(err);  // every peer has imported our handles
     }
 
@@ -1119,6 +1193,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     HIP_TRY(hipMemset(s.dev_epochs, 0, kMaxTeams * sizeof(uint32_t)));
     if (sync_device_ctx(s)) return 1;
     s.initialized = true;
+    write_ctx_slots(s.dctx);
     return 0;
 }
 
@@ -1170,6 +1245,7 @@ int ishmemi_c_finalize(void)
     std::lock_guard<std::mutex> lk(s.mu);
     if (!s.initialized) return 0;
     (void) hipDeviceSynchronize();
+    write_ctx_slots(nullptr);  // device-API calls after finalize fail instead of using freed state
     if (s.npes > 1) {
         std::string err;
         s.boot.barrier(err);  // no peer may still be reading our heap
@@ -1216,6 +1292,35 @@ int ishmemi_c_finalize(void)
 }
 
 int ishmemi_c_initialized(void) { return S().initialized ? 1 : 0; }
+
+int ishmemi_c_register_device_ctx_slot(const void *host_shadow)
+{
+    if (!host_shadow) return 0;
+    {
+        CtxSlots &c = ctx_slots();
+        std::lock_guard<std::mutex> lk(c.mu);
+        c.shadows.push_back(host_shadow);
+    }
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (s.initialized) write_ctx_slot(host_shadow, s.dctx);  // a code object loaded after init
+    return 0;
+}
+
+int ishmemi_c_init_thread(int requested, int *provided)
+{
+    // src/ishmem.cpp:409-419: always ISHMEM_THREAD_MULTIPLE (host calls are serialised here).
+    (void) requested;
+    const int r = ishmemi_c_init();
+    if (provided) *provided = ISHMEMI_C_THREAD_MULTIPLE;
+    return r;
+}
+
+int ishmemi_c_query_thread(int *provided)
+{
+    if (provided) *provided = ISHMEMI_C_THREAD_MULTIPLE;
+    return S().initialized ? 0 : fail("query_thread: not initialized");
+}
 int ishmemi_c_my_pe(void) { return S().initialized ? S().pe : -1; }
 int ishmemi_c_n_pes(void) { return S().initialized ? S().npes : -1; }
 int ishmemi_c_device(void) { return S().initialized ? S().device : -1; }
@@ -1413,6 +1518,31 @@ int ishmemi_c_team_split_2d(int parent, int xrange, int *xaxis_team, int *yaxis_
     return 0;
 }
 
+int ishmemi_c_team_get_config(int team, long config_mask, int *num_contexts)
+{
+    // src/teams.cpp:545-570: mask 0 reports nothing; mask ISHMEM_TEAM_NUM_CONTEXTS needs the pointer.
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.initialized) return fail("team_get_config: not initialized");
+    if (team < 0 || team >= kMaxTeams || !s.teams[team].valid) return fail("team_get_config: invalid team");
+    if (config_mask == 0) return 0;
+    if (config_mask != 1) return fail("team_get_config: invalid config mask");
+    if (!num_contexts) return fail("team_get_config: NULL config with a nonzero mask");
+    *num_contexts = s.teams[team].num_contexts;
+    return 0;
+}
+
+int ishmemi_c_team_set_config(int team, long config_mask, int num_contexts)
+{
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.initialized) return fail("team_set_config: not initialized");
+    if (team < 0 || team >= kMaxTeams || !s.teams[team].valid) return fail("team_set_config: invalid team");
+    if (config_mask != 0 && config_mask != 1) return fail("team_set_config: invalid config mask");
+    if (config_mask) s.teams[team].num_contexts = num_contexts;
+    return 0;
+}
+
 void ishmemi_c_team_destroy(int team)
 {
     State &s = S();
@@ -1595,7 +1725,20 @@ int ishmemi_c_occupy(int grid, unsigned long long usec, void *stream)
 
 int ishmemi_c_fcollect(int team, void *dest, const void *source, size_t nbytes)
 {
-    return fcollect_impl(team, dest, source, nbytes, nullptr, 0, true);
+    // Members agree on the staged path (any member's source outside the heap: all stage) and on
+    // argument failures before anything is launched.
+    State &s = S();
+    int staged = -1;
+    if (member_call(s, team) && s.teams[team].size > 1 && nbytes > 0) {
+        const uint64_t mine = (in_heap(s, source) ? 0 : kAgreeStaged) | (device_writable(s, dest) ? 0 : kAgreeFail);
+        uint64_t all[kMaxPes], any = 0;
+        if (team_exchange(team, mine, all)) return 1;
+        for (int j = 0; j < s.teams[team].size; ++j) any |= all[j];
+        if (any & kAgreeFail)
+            return fail("fcollect: a member's dest is not device-writable (heap, device or pinned host memory)");
+        staged = (any & kAgreeStaged) ? 1 : 0;
+    }
+    return fcollect_impl(team, dest, source, nbytes, nullptr, 0, true, staged);
 }
 
 int ishmemi_c_fcollect_on_stream(int team, void *dest, const void *source, size_t nbytes, int *ret,
@@ -1614,23 +1757,20 @@ int ishmemi_c_collect(int team, void *dest, const void *source, size_t nbytes)
         return fail("collect: invalid team or caller not a member");
     const int p = s.teams[team].size;
     if (p == 1) return ishmemi_c_fcollect(team, dest, source, nbytes);
-    // Bit 63 of a count: that member's source is outside the heap; then every member takes the
-    // staged path (peers' sources are only found from a symmetric source address).
-    constexpr uint64_t kStagedBit = 1ull << 63;
-    const uint64_t mine = nbytes | (in_heap(s, source) ? 0 : kStagedBit);
-    if (hipMemcpy(s.team_scratch, &mine, 8, hipMemcpyHostToDevice) != hipSuccess)
-        return fail("collect: count copy failed");
-    if (ishmemi_c_fcollect(team, s.team_scratch + 64, s.team_scratch, 8)) return 1;
+    // With the count: kAgreeStaged = that member's source is outside the heap (then every member
+    // takes the staged path: peers' sources are only found from a symmetric source address);
+    // kAgreeFail = its dest is not device-writable (then every member fails, nothing launched).
+    const uint64_t mine = nbytes | (in_heap(s, source) ? 0 : kAgreeStaged) | (device_writable(s, dest) ? 0 : kAgreeFail);
     uint64_t counts[kMaxPes];
-    if (hipMemcpy(counts, s.team_scratch + 64, 8 * (size_t) p, hipMemcpyDeviceToHost) != hipSuccess)
-        return fail("collect: count copy failed");
-    bool staged = false;
+    if (team_exchange(team, mine, counts)) return 1;
+    bool staged = false, failed = false;
     for (int j = 0; j < p; ++j) {
-        staged = staged || (counts[j] & kStagedBit);
-        counts[j] &= ~kStagedBit;
+        staged = staged || (counts[j] & kAgreeStaged);
+        failed = failed || (counts[j] & kAgreeFail);
+        counts[j] &= ~(kAgreeStaged | kAgreeFail);
     }
+    if (failed) return fail("collect: a member's dest is not device-writable (heap, device or pinned host memory)");
     std::lock_guard<std::mutex> lk(s.mu);
-    if (!device_writable(s, dest)) return fail("collect: dest must be heap, device or pinned host memory");
     if (staged) {
         if (order_stream(s, 0) || collect_staged(s, team, (char *) dest, (const char *) source, counts, nullptr, 0))
             return 1;
@@ -1651,31 +1791,79 @@ int ishmemi_c_collect_on_stream(int team, void *dest, const void *source, size_t
 int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *source, size_t nelems)
 {
     // Buffers outside the heap (the reference proxies host buffers to MPI_Scan / MPI_Exscan,
-    // runtime_mpi.cpp:816-835): through symmetric temporaries, copied in / out around the device
-    // scan.  The allocator is deterministic, so members that all pass non-heap buffers of the same
-    // length get temporaries at the same offsets (every member must pass the same kind).
+    // runtime_mpi.cpp:816-835) go through symmetric temporaries, copied in / out around the device
+    // scan.  The members first agree (team_exchange) whether ANY of them needs temporaries; if so
+    // every member allocates both, in the same order, from an allocator in the same state (all
+    // other allocations are collective), so the source temporaries sit at the same offset on
+    // every member, which the scan kernel requires.  Callers serialise collectives per team, as in
+    // the reference (src/teams.h:29-38).
     State &s = S();
-    char *ts = nullptr, *td = nullptr;
     const size_t bytes = nelems * dtype_size(dtype);
-    if (s.initialized && nelems && team >= 0 && team < kMaxTeams && s.teams[team].valid &&
-        s.teams[team].size > 1 && (!in_heap(s, dest) || !in_heap(s, source))) {
-        {
-            std::lock_guard<std::mutex> lk(s.mu);
-            ts = in_heap(s, source) ? (char *) source : (char *) heap_alloc(s, bytes, 256);
-            td = in_heap(s, dest) ? (char *) dest : (char *) heap_alloc(s, bytes, 256);
-        }
-        int rc = (!ts || !td) ? 1 : 0;
-        if (!rc && ts != source && hipMemcpy(ts, source, bytes, hipMemcpyDefault) != hipSuccess)
-            rc = fail("scan: staging copy-in failed");
-        if (!rc) rc = scan_impl(team, dtype, inclusive, td, ts, nelems, nullptr, 0, true);
-        if (!rc && td != dest && hipMemcpy(dest, td, bytes, hipMemcpyDefault) != hipSuccess)
-            rc = fail("scan: staging copy-out failed");
+    if (!member_call(s, team) || nelems == 0 || s.teams[team].size == 1 || !op_dtype_valid(ISHMEMI_OP_SUM, dtype))
+        return scan_impl(team, dtype, inclusive, dest, source, nelems, nullptr, 0, true);
+    const uint64_t mine = (in_heap(s, source) && in_heap(s, dest)) ? 0 : kAgreeStaged;
+    uint64_t all[kMaxPes], any = 0;
+    if (team_exchange(team, mine, all)) return 1;
+    for (int j = 0; j < s.teams[team].size; ++j) any |= all[j];
+    if (!(any & kAgreeStaged)) return scan_impl(team, dtype, inclusive, dest, source, nelems, nullptr, 0, true);
+    char *ts, *td;
+    {
         std::lock_guard<std::mutex> lk(s.mu);
-        if (ts && ts != source) heap_free(s, ts);
-        if (td && td != dest) heap_free(s, td);
-        return rc;
+        ts = (char *) heap_alloc(s, bytes, 256);
+        td = (char *) heap_alloc(s, bytes, 256);
     }
-    return scan_impl(team, dtype, inclusive, dest, source, nelems, nullptr, 0, true);
+    int rc = (!ts || !td) ? 1 : 0;  // the same outcome on every member (same allocator state)
+    if (!rc && hipMemcpy(ts, source, bytes, hipMemcpyDefault) != hipSuccess) rc = fail("scan: staging copy-in failed");
+    char *d = in_heap(s, dest) ? (char *) dest : td;
+    if (!rc) rc = scan_impl(team, dtype, inclusive, d, ts, nelems, nullptr, 0, true);
+    if (!rc && d != dest && hipMemcpy(dest, d, bytes, hipMemcpyDefault) != hipSuccess)
+        rc = fail("scan: staging copy-out failed");
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (td) heap_free(s, td);
+    if (ts) heap_free(s, ts);
+    return rc;
+}
+
+int ishmemi_c_broadcast(int team, void *dest, const void *source, size_t nbytes, int root)
+{
+    // The reference's intra-node pull (broadcast_impl.h: team sync, every member gets the root's
+    // source, team sync) on the collect kernel: only the root contributes, every member's dest
+    // receives it at offset 0.  The members exchange the root's source offset in the heap (its
+    // source is found from it, whatever the others pass), whether it must be staged (outside the
+    // heap) and any local argument failure, before anything is launched.
+    State &s = S();
+    if (!member_call(s, team)) return fail("broadcast: not initialized, invalid team or caller not a member");
+    const int p = s.teams[team].size;
+    if (root < 0 || root >= p) return fail("broadcast: root is not a team index");
+    if (p == 1) {  // the root alone: dest = source, from or to any kind of memory
+        if (nbytes && dest != source) HIP_TRY(hipMemcpy(dest, source, nbytes, hipMemcpyDefault));
+        return 0;
+    }
+    const Team &t = s.teams[team];
+    const bool me_root = t.my_idx == root;
+    uint64_t mine = 0;
+    if (me_root) mine = in_heap(s, source) ? (uint64_t) ((const char *) source - s.heap) : kAgreeStaged;
+    if (nbytes && !device_writable(s, dest)) mine |= kAgreeFail;
+    uint64_t all[kMaxPes], any = 0;
+    if (team_exchange(team, mine, all)) return 1;
+    for (int j = 0; j < p; ++j) any |= all[j];
+    if (any & kAgreeFail) return fail("broadcast: a member's dest is not device-writable (heap, device or pinned host memory)");
+    if (nbytes == 0) return ishmemi_c_team_sync(team);
+    uint64_t counts[kMaxPes] = {}, zero[kMaxPes] = {};
+    counts[root] = nbytes;
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (all[root] & kAgreeStaged) {
+        if (order_stream(s, 0) || collect_staged(s, team, (char *) dest, (const char *) source, counts, nullptr, 0))
+            return 1;
+    } else {
+        const char *srcs[kMaxPes];
+        const int groot = t.start + root * t.stride;
+        for (int j = 0; j < p; ++j) srcs[j] = s.peer_heap[groot] + all[root];
+        if (collect_launch(s, team, dest, nullptr, counts, nullptr, 0, zero, srcs)) return 1;
+    }
+    if (mark_stream(s, 0)) return 1;
+    HIP_TRY(hipStreamSynchronize(0));
+    return check_team_errors(s, team);
 }
 
 int ishmemi_c_scan_on_stream(int team, int dtype, int inclusive, void *dest, const void *source,

@@ -5,7 +5,12 @@
 // reference check patterns restated in oracle/oracle.c, linked here as the CHECKER).
 // Also: a wavefront (sub_group) caller and a single work-item device-side ishmem_int_sum_reduce,
 // and the device-side fcollect / collect / sum_inscan / sum_exscan (closed-form checks).
+// Every device call is the reference's context-free form (the library's device state reaches the
+// kernels through include/ishmemx_device.h's per-code-object context slot); groups are HIP
+// cooperative groups (thread_block for sycl::group, a 64-lane thread_block_tile for sub_group) or
+// the library's tags.
 // Launch: ISHMEM_PE=<pe> ISHMEM_NPES=<n> ISHMEM_DEVICE=0 ISHMEM_BOOTSTRAP_KEY=<k> ./device_wg
+#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -13,7 +18,9 @@
 #include <vector>
 
 #include "ishmem.h"
-#include "ishmemx_device.h"
+#include "ishmemx.h"
+
+namespace cg = cooperative_groups;
 
 extern "C" {
 #include "oracle.h"
@@ -22,95 +29,96 @@ extern "C" {
 static int errors = 0;
 
 // long_reduce.cpp:78-79 / :120-127 — produce, then reduce, in one kernel.
-__global__ void long_reduce_kernel(const ishmemi_c_device_ctx_t *ctx, long *dest, long *source,
+__global__ void long_reduce_kernel(long *dest, long *source,
                                    size_t n, int my_pe, int *rc)
 {
     for (size_t i = threadIdx.x; i < n; i += blockDim.x) source[i] = (1L << (40 + my_pe)) + (long) i;
-    const int r = ishmemx_long_sum_reduce_work_group(ctx, dest, (const long *) source, n);
+    const int r = ishmemx_long_sum_reduce_work_group(dest, (const long *) source, n, cg::this_thread_block());
     if (threadIdx.x == 0) *rc = r;
 }
 
 template <typename T, int OPC>
-__global__ void pattern_kernel(const ishmemi_c_device_ctx_t *ctx, int team, T *dest, const T *source,
+__global__ void pattern_kernel(int team, T *dest, const T *source,
                                size_t n, int *rc)
 {
     int r;
-    if constexpr (OPC == ISHMEMI_OP_SUM) r = ishmemx_sum_reduce_work_group(ctx, team, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_MAX) r = ishmemx_max_reduce_work_group(ctx, team, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_MIN) r = ishmemx_min_reduce_work_group(ctx, team, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_PROD) r = ishmemx_prod_reduce_work_group(ctx, team, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_AND) r = ishmemx_and_reduce_work_group(ctx, team, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_OR) r = ishmemx_or_reduce_work_group(ctx, team, dest, source, n);
-    else r = ishmemx_xor_reduce_work_group(ctx, team, dest, source, n);
+    if constexpr (OPC == ISHMEMI_OP_SUM) r = ishmemx_sum_reduce_work_group(team, dest, source, n, cg::this_thread_block());
+    else if constexpr (OPC == ISHMEMI_OP_MAX) r = ishmemx_max_reduce_work_group(team, dest, source, n, cg::this_thread_block());
+    else if constexpr (OPC == ISHMEMI_OP_MIN) r = ishmemx_min_reduce_work_group(team, dest, source, n, cg::this_thread_block());
+    else if constexpr (OPC == ISHMEMI_OP_PROD) r = ishmemx_prod_reduce_work_group(team, dest, source, n, cg::this_thread_block());
+    else if constexpr (OPC == ISHMEMI_OP_AND) r = ishmemx_and_reduce_work_group(team, dest, source, n, cg::this_thread_block());
+    else if constexpr (OPC == ISHMEMI_OP_OR) r = ishmemx_or_reduce_work_group(team, dest, source, n, cg::this_thread_block());
+    else r = ishmemx_xor_reduce_work_group(team, dest, source, n, cg::this_thread_block());
     if (threadIdx.x == 0) *rc = r;
 }
 
 // The reference CTest's "device" mode (test/unit/CMakeLists.txt:35, ishmem_tester.h:1229-1232):
 // the blocking ishmem_<op>_reduce called by ONE work-item inside a kernel.
 template <typename T, int OPC>
-__global__ void device_mode_kernel(const ishmemi_c_device_ctx_t *ctx, T *dest, const T *source, size_t n,
+__global__ void device_mode_kernel(T *dest, const T *source, size_t n,
                                    int *rc)
 {
     int r;
-    if constexpr (OPC == ISHMEMI_OP_SUM) r = ishmem_sum_reduce(ctx, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_MAX) r = ishmem_max_reduce(ctx, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_MIN) r = ishmem_min_reduce(ctx, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_PROD) r = ishmem_prod_reduce(ctx, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_AND) r = ishmem_and_reduce(ctx, dest, source, n);
-    else if constexpr (OPC == ISHMEMI_OP_OR) r = ishmem_or_reduce(ctx, dest, source, n);
-    else r = ishmem_xor_reduce(ctx, dest, source, n);
+    if constexpr (OPC == ISHMEMI_OP_SUM) r = ishmem_sum_reduce(dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_MAX) r = ishmem_max_reduce(dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_MIN) r = ishmem_min_reduce(dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_PROD) r = ishmem_prod_reduce(dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_AND) r = ishmem_and_reduce(dest, source, n);
+    else if constexpr (OPC == ISHMEMI_OP_OR) r = ishmem_or_reduce(dest, source, n);
+    else r = ishmem_xor_reduce(dest, source, n);
     *rc = r;
 }
 
 // long_reduce.cpp:145-186: the in-place variant (source == dest) of the produce-then-reduce kernel.
-__global__ void long_reduce_inplace_kernel(const ishmemi_c_device_ctx_t *ctx, long *buf, size_t n, int my_pe,
+__global__ void long_reduce_inplace_kernel(long *buf, size_t n, int my_pe,
                                            int *rc)
 {
     for (size_t i = threadIdx.x; i < n; i += blockDim.x) buf[i] = (1L << (40 + my_pe)) + (long) i;
-    const int r = ishmemx_long_sum_reduce_work_group(ctx, buf, (const long *) buf, n);
+    const int r = ishmemx_long_sum_reduce_work_group(buf, (const long *) buf, n, ishmemx_dev::work_group);
     if (threadIdx.x == 0) *rc = r;
 }
 
 // sub_group analogue: only the second wavefront of the work-group takes part.
-__global__ void wave_kernel(const ishmemi_c_device_ctx_t *ctx, float *dest, const float *source, size_t n,
+__global__ void wave_kernel(float *dest, const float *source, size_t n,
                             int *rc)
 {
     if (threadIdx.x / warpSize != 1) return;
-    const int r = ishmemx_float_sum_reduce_work_group(ctx, dest, source, n, ishmemx_dev::wavefront);
+    const int r = ishmemx_float_sum_reduce_work_group(dest, source, n, ishmemx_dev::wavefront);
     if (__lane_id() == 0) *rc = r;
 }
 
 // Device-side blocking call by one work-item (the reference's single_task shape).
-__global__ void single_kernel(const ishmemi_c_device_ctx_t *ctx, int *dest, const int *source, size_t n,
+__global__ void single_kernel(int *dest, const int *source, size_t n,
                               int *rc)
 {
-    *rc = ishmem_int_sum_reduce(ctx, ISHMEM_TEAM_WORLD, dest, source, n);
+    *rc = ishmem_int_sum_reduce(ISHMEM_TEAM_WORLD, dest, source, n);
 }
 
 // Device-side fcollect / collect / sum-scan (src/ishmemx.h *_work_group): the source is produced
 // in the same kernel, then the collective runs by the work-group (or one wavefront / one item).
 template <int MODE>  // 0 fcollect, 1 collect, 2 inscan, 3 exscan, 4 fcollect by a wavefront,
                      // 5 inscan by one work-item
-__global__ void coll_kernel(const ishmemi_c_device_ctx_t *ctx, long *dest, long *source, size_t n, int my_pe,
+__global__ void coll_kernel(long *dest, long *source, size_t n, int my_pe,
                             int *rc)
 {
     const size_t mine = MODE == 1 ? n + 37 * (size_t) my_pe : n;  // collect: counts differ per PE
     for (size_t i = threadIdx.x; i < mine; i += blockDim.x) source[i] = ((long) (my_pe + 1) << 32) + (long) i;
     int r = 0;
-    if constexpr (MODE == 0) r = ishmemx_long_fcollect_work_group(ctx, dest, (const long *) source, n);
-    else if constexpr (MODE == 1) r = ishmemx_long_collect_work_group(ctx, dest, (const long *) source, mine);
-    else if constexpr (MODE == 2) r = ishmemx_long_sum_inscan_work_group(ctx, dest, (const long *) source, n);
-    else if constexpr (MODE == 3) r = ishmemx_long_sum_exscan_work_group(ctx, dest, (const long *) source, n);
+    if constexpr (MODE == 0) r = ishmemx_long_fcollect_work_group(dest, (const long *) source, n, cg::this_thread_block());
+    else if constexpr (MODE == 1) r = ishmemx_long_collect_work_group(dest, (const long *) source, mine, cg::this_thread_block());
+    else if constexpr (MODE == 2) r = ishmemx_long_sum_inscan_work_group(dest, (const long *) source, n, cg::this_thread_block());
+    else if constexpr (MODE == 3) r = ishmemx_long_sum_exscan_work_group(dest, (const long *) source, n, cg::this_thread_block());
     else if constexpr (MODE == 4) {
         __syncthreads();  // every wave's source stores are done before one wavefront publishes them
+        auto wave = cg::tiled_partition<64>(cg::this_thread_block());  // sub_group analogue
         if (threadIdx.x / warpSize != 0) return;
-        r = ishmemx_long_fcollect_work_group(ctx, dest, (const long *) source, n, ishmemx_dev::wavefront);
+        r = ishmemx_long_fcollect_work_group(dest, (const long *) source, n, wave);
         if (__lane_id() == 0) *rc = r;
         return;
     } else {
         __syncthreads();
         if (threadIdx.x != 0) return;
-        r = ishmem_long_sum_inscan(ctx, ISHMEM_TEAM_WORLD, dest, (const long *) source, n);
+        r = ishmem_long_sum_inscan(ISHMEM_TEAM_WORLD, dest, (const long *) source, n);
         *rc = r;
         return;
     }
@@ -118,7 +126,7 @@ __global__ void coll_kernel(const ishmemi_c_device_ctx_t *ctx, long *dest, long 
 }
 
 template <int MODE>
-static void coll_case(const ishmemi_c_device_ctx_t *ctx, size_t n, int block, char *sb, char *db, int *rc)
+static void coll_case(size_t n, int block, char *sb, char *db, int *rc)
 {
     const int pe = ishmem_my_pe(), npes = ishmem_n_pes();
     auto val = [](int j, size_t i) { return ((long) (j + 1) << 32) + (long) i; };
@@ -138,7 +146,7 @@ static void coll_case(const ishmemi_c_device_ctx_t *ctx, size_t n, int block, ch
     }
     (void) hipMemset(db, 0xA5, want.size() * sizeof(long) + 64);
     (void) hipMemset(rc, 0xff, sizeof(int));
-    hipLaunchKernelGGL(coll_kernel<MODE>, dim3(1), dim3(block), 0, 0, ctx, (long *) db, (long *) sb, n, pe, rc);
+    hipLaunchKernelGGL(coll_kernel<MODE>, dim3(1), dim3(block), 0, 0, (long *) db, (long *) sb, n, pe, rc);
     (void) hipDeviceSynchronize();
     int r = -1;
     std::vector<long> got(want.size() + 8);
@@ -155,7 +163,7 @@ static void coll_case(const ishmemi_c_device_ctx_t *ctx, size_t n, int block, ch
 }
 
 template <typename K, typename T, int OPC, int ODT>
-static void group_case(const char *what, K kernel, int block, const ishmemi_c_device_ctx_t *ctx, size_t n,
+static void group_case(const char *what, K kernel, int block, size_t n,
                        char *sb, char *db, int *rc)
 {
     const int pe = ishmem_my_pe(), npes = ishmem_n_pes();
@@ -165,7 +173,7 @@ static void group_case(const char *what, K kernel, int block, const ishmemi_c_de
     (void) hipMemcpy(sb, src.data(), n * sizeof(T), hipMemcpyHostToDevice);
     (void) hipMemset(db, 0, n * sizeof(T));
     (void) hipMemset(rc, 0xff, sizeof(int));
-    hipLaunchKernelGGL(kernel, dim3(1), dim3(block), 0, 0, ctx, (T *) db, (const T *) sb, n, rc);
+    hipLaunchKernelGGL(kernel, dim3(1), dim3(block), 0, 0, (T *) db, (const T *) sb, n, rc);
     (void) hipDeviceSynchronize();
     int r = -1;
     (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);
@@ -176,7 +184,7 @@ static void group_case(const char *what, K kernel, int block, const ishmemi_c_de
 }
 
 template <typename T, int OPC, int ODT>
-static void pattern_case(const ishmemi_c_device_ctx_t *ctx, size_t n, dim3 block, char *sb, char *db,
+static void pattern_case(size_t n, dim3 block, char *sb, char *db,
                          int *rc, bool single_item = false)
 {
     const int pe = ishmem_my_pe(), npes = ishmem_n_pes();
@@ -187,10 +195,10 @@ static void pattern_case(const ishmemi_c_device_ctx_t *ctx, size_t n, dim3 block
     (void) hipMemcpy(sb, src.data(), n * sizeof(T), hipMemcpyHostToDevice);
     (void) hipMemset(db, 0, n * sizeof(T));
     if (single_item)
-        hipLaunchKernelGGL((device_mode_kernel<T, OPC>), dim3(1), dim3(1), 0, 0, ctx, (T *) db, (const T *) sb,
+        hipLaunchKernelGGL((device_mode_kernel<T, OPC>), dim3(1), dim3(1), 0, 0, (T *) db, (const T *) sb,
                            n, rc);
     else
-        hipLaunchKernelGGL((pattern_kernel<T, OPC>), dim3(1), block, 0, 0, ctx, ISHMEM_TEAM_WORLD,
+        hipLaunchKernelGGL((pattern_kernel<T, OPC>), dim3(1), block, 0, 0, ISHMEM_TEAM_WORLD,
                            (T *) db, (const T *) sb, n, rc);
     (void) hipDeviceSynchronize();
     int r = -1;
@@ -211,7 +219,6 @@ int main()
         printf("init failed: %s\n", ishmemi_c_last_error());
         return 2;
     }
-    const auto *ctx = (const ishmemi_c_device_ctx_t *) ishmemi_c_device_ctx();
     const size_t maxn = 1 << 17;
     char *sb = (char *) ishmem_malloc(maxn * 8);
     char *db = (char *) ishmem_malloc(maxn * 8);
@@ -219,7 +226,7 @@ int main()
 
     for (size_t n = 1; n <= maxn; n <<= 2) {
         for (int block : {64, 256, 1024}) {
-            hipLaunchKernelGGL(long_reduce_kernel, dim3(1), dim3(block), 0, 0, ctx, (long *) db, (long *) sb,
+            hipLaunchKernelGGL(long_reduce_kernel, dim3(1), dim3(block), 0, 0, (long *) db, (long *) sb,
                                n, pe, rc);
             (void) hipDeviceSynchronize();
             std::vector<long> got(n);
@@ -235,18 +242,18 @@ int main()
         }
     }
     for (size_t n : {1, 7, 64, 1000, 4097}) {
-        pattern_case<float, OR_SUM, OD_FLOAT>(ctx, n, 256, sb, db, rc);
-        pattern_case<double, OR_PROD, OD_DOUBLE>(ctx, n, 256, sb, db, rc);
-        pattern_case<int32_t, OR_MIN, OD_INT32>(ctx, n, 128, sb, db, rc);
-        pattern_case<int8_t, OR_MAX, OD_INT8>(ctx, n, 256, sb, db, rc);
-        pattern_case<int16_t, OR_SUM, OD_INT16>(ctx, n, 64, sb, db, rc);
-        pattern_case<uint64_t, OR_XOR, OD_UINT64>(ctx, n, 512, sb, db, rc);
-        pattern_case<uint8_t, OR_AND, OD_UINT8>(ctx, n, 256, sb, db, rc);
-        pattern_case<uint32_t, OR_OR, OD_UINT32>(ctx, n, 256, sb, db, rc);
+        pattern_case<float, OR_SUM, OD_FLOAT>(n, 256, sb, db, rc);
+        pattern_case<double, OR_PROD, OD_DOUBLE>(n, 256, sb, db, rc);
+        pattern_case<int32_t, OR_MIN, OD_INT32>(n, 128, sb, db, rc);
+        pattern_case<int8_t, OR_MAX, OD_INT8>(n, 256, sb, db, rc);
+        pattern_case<int16_t, OR_SUM, OD_INT16>(n, 64, sb, db, rc);
+        pattern_case<uint64_t, OR_XOR, OD_UINT64>(n, 512, sb, db, rc);
+        pattern_case<uint8_t, OR_AND, OD_UINT8>(n, 256, sb, db, rc);
+        pattern_case<uint32_t, OR_OR, OD_UINT32>(n, 256, sb, db, rc);
     }
     // In place (long_reduce.cpp:145-186).
     for (size_t n : {1, 100, 4096, 65536}) {
-        hipLaunchKernelGGL(long_reduce_inplace_kernel, dim3(1), dim3(256), 0, 0, ctx, (long *) sb, n, pe, rc);
+        hipLaunchKernelGGL(long_reduce_inplace_kernel, dim3(1), dim3(256), 0, 0, (long *) sb, n, pe, rc);
         (void) hipDeviceSynchronize();
         std::vector<long> got(n);
         int r = -1;
@@ -261,7 +268,7 @@ int main()
     }
     // "device" mode (one work-item) over every valid (op, dtype) with the testers' patterns.
     for (size_t n : {1, 17, 129}) {
-#define DM(T, OPC, ODT) pattern_case<T, OPC, ODT>(ctx, n, dim3(1), sb, db, rc, true);
+#define DM(T, OPC, ODT) pattern_case<T, OPC, ODT>(n, dim3(1), sb, db, rc, true);
 #define DM_INT(OPC) DM(int8_t, OPC, OD_INT8) DM(int16_t, OPC, OD_INT16) DM(int32_t, OPC, OD_INT32) \
     DM(int64_t, OPC, OD_INT64) DM(uint8_t, OPC, OD_UINT8) DM(uint16_t, OPC, OD_UINT16) DM(uint32_t, OPC, OD_UINT32) \
     DM(uint64_t, OPC, OD_UINT64)
@@ -274,25 +281,25 @@ int main()
     }
     // device_grp2 / device_grp3: 2-D and 3-D work-groups (team_reduce_test.h TEST_GRP2_FN / GRP3).
     for (size_t n : {1, 1000, 4097}) {
-        pattern_case<float, OR_SUM, OD_FLOAT>(ctx, n, dim3(16, 16), sb, db, rc);
-        pattern_case<int64_t, OR_MAX, OD_INT64>(ctx, n, dim3(8, 4, 8), sb, db, rc);
-        pattern_case<uint16_t, OR_XOR, OD_UINT16>(ctx, n, dim3(32, 2, 2), sb, db, rc);
+        pattern_case<float, OR_SUM, OD_FLOAT>(n, dim3(16, 16), sb, db, rc);
+        pattern_case<int64_t, OR_MAX, OD_INT64>(n, dim3(8, 4, 8), sb, db, rc);
+        pattern_case<uint16_t, OR_XOR, OD_UINT16>(n, dim3(32, 2, 2), sb, db, rc);
     }
     for (size_t n : {1, 63, 64, 1000, 20000}) {
-        group_case<decltype(&wave_kernel), float, OR_SUM, OD_FLOAT>("wavefront float sum", wave_kernel, 256, ctx,
-                                                                    n, sb, db, rc);
-        group_case<decltype(&single_kernel), int, OR_SUM, OD_INT32>("single-thread int sum", single_kernel, 1,
-                                                                    ctx, n, sb, db, rc);
+        group_case<decltype(&wave_kernel), float, OR_SUM, OD_FLOAT>("wavefront float sum", wave_kernel, 256, n, sb,
+                                                                    db, rc);
+        group_case<decltype(&single_kernel), int, OR_SUM, OD_INT32>("single-thread int sum", single_kernel, 1, n,
+                                                                    sb, db, rc);
     }
     // fcollect / collect / inscan / exscan from inside a kernel (dest room: npes * (n + 37 npes)).
     for (size_t n : {1, 5, 64, 1000, 4099}) {
         if ((size_t) npes * (n + 37 * (size_t) npes) + 16 > maxn) continue;
-        coll_case<0>(ctx, n, 256, sb, db, rc);
-        coll_case<1>(ctx, n, 256, sb, db, rc);
-        coll_case<2>(ctx, n, 256, sb, db, rc);
-        coll_case<3>(ctx, n, 1024, sb, db, rc);
-        coll_case<4>(ctx, n, 128, sb, db, rc);
-        coll_case<5>(ctx, n, 64, sb, db, rc);
+        coll_case<0>(n, 256, sb, db, rc);
+        coll_case<1>(n, 256, sb, db, rc);
+        coll_case<2>(n, 256, sb, db, rc);
+        coll_case<3>(n, 1024, sb, db, rc);
+        coll_case<4>(n, 128, sb, db, rc);
+        coll_case<5>(n, 64, sb, db, rc);
     }
     ishmem_free(rc);
     ishmem_free(db);

@@ -24,11 +24,11 @@
 #include "ishmemx_device.h"
 
 template <typename G>
-__global__ void wg_loop(const ishmemi_c_device_ctx_t *ctx, long *dest, const long *src, size_t n,
+__global__ void wg_loop(long *dest, const long *src, size_t n,
                         size_t iters, int *rc)
 {
     int bad = 0;
-    for (size_t i = 0; i < iters; ++i) bad |= ishmemx_long_sum_reduce_work_group(ctx, dest, src, n, G());
+    for (size_t i = 0; i < iters; ++i) bad |= ishmemx_long_sum_reduce_work_group(dest, src, n, G());
     if (threadIdx.x == 0) *rc = bad;
 }
 
@@ -60,7 +60,6 @@ int main(int argc, char **argv)
     hipStream_t st;
     (void) hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     (void) hipMemset(src, 1, max_nelems * sizeof(long));
-    const ishmemi_c_device_ctx_t *ctx = (const ishmemi_c_device_ctx_t *) ishmemi_c_device_ctx();
     if (csv && me == 0) printf("csv,testname,ipc,npes,type,op,mode,groups,threads,bytes,pe,latency_us,bw_mb\n");
 
     const char *modes[] = {"host_device_device", "on_queue", "device_grp1", "device_subgroup"};
@@ -80,11 +79,11 @@ int main(int argc, char **argv)
                     (void) hipStreamSynchronize(st);
                 } else {
                     if (wave)
-                        hipLaunchKernelGGL(wg_loop<ishmemx_dev::wavefront_t>, dim3(1), dim3(64), 0, st, ctx,
+                        hipLaunchKernelGGL(wg_loop<ishmemx_dev::wavefront_t>, dim3(1), dim3(64), 0, st,
                                            dst, (const long *) src, n, iters, rc);
                     else
                         hipLaunchKernelGGL(wg_loop<ishmemx_dev::work_group_t>, dim3(1), dim3(1024), 0, st,
-                                           ctx, dst, (const long *) src, n, iters, rc);
+                                           dst, (const long *) src, n, iters, rc);
                     (void) hipStreamSynchronize(st);
                     int r = 0;
                     (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);

@@ -31,6 +31,25 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
         import ishmem_amd as ish
         from ishmem_amd import hip
 
+        if "refuse" in scenarios:
+            # Coarse-grained flag memory across devices (ISHMEM_TEST_FLAGS_UNAVAILABLE: as if no
+            # uncached / fine-grained VRAM could be shared; ISHMEM_TEST_PCI_BUS: each PE claims its
+            # own device): init must fail on every PE with the reason, not warn and continue.
+            # With ISHMEM_FLAGS_KIND=2 (a test forcing coarse-grained flags) it must succeed.
+            forced = os.environ.get("ISHMEM_FLAGS_KIND") == "2"
+            try:
+                ish.init(pe, npes, 0, key)
+                if not forced:
+                    fails.append(f"pe{pe} refuse: init succeeded with coarse-grained flags across devices")
+                elif int(ish.get_param("flags_kind")) != 2:
+                    fails.append(f"pe{pe} refuse (forced): flags_kind {ish.get_param('flags_kind')}")
+                ish.ishmem_finalize()
+            except RuntimeError as ex:
+                if forced or "coarse-grained" not in str(ex):
+                    fails.append(f"pe{pe} refuse: unexpected init outcome: {ex}")
+            q.put((pe, fails))
+            return
+
         ish.init(pe, npes, 0, key)
         OPS, DT = oracle.OPS, oracle.DTYPES
         NAMES = {v: k for k, v in DT.items()}
@@ -116,6 +135,102 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             ish.ishmem_finalize()
             q.put((pe, fails))
             return
+
+        if "setup" in scenarios:
+            # The setup surface of src/ishmem.h:23-26, :44-45, :57-58, :78 (threading, version /
+            # name, team configuration).
+            if ish.ishmem_query_thread() != ish.ISHMEM_THREAD_MULTIPLE:
+                fails.append(f"pe{pe} query_thread {ish.ishmem_query_thread()}")
+            if ish.ishmem_info_get_version() != (1, 5) or not ish.ishmem_info_get_name():
+                fails.append(f"pe{pe} info_get")
+            if ish.ishmem_team_get_config(ish.ISHMEM_TEAM_WORLD) != (0, 0):
+                fails.append(f"pe{pe} team_get_config WORLD {ish.ishmem_team_get_config(ish.ISHMEM_TEAM_WORLD)}")
+            if ish.lib().ishmemi_c_team_get_config(ish.ISHMEM_TEAM_WORLD, 1, None) == 0:
+                fails.append(f"pe{pe} team_get_config accepted a NULL config with a nonzero mask")
+            if ish.lib().ishmemi_c_team_get_config(ish.ISHMEM_TEAM_WORLD, 0, None) != 0:
+                fails.append(f"pe{pe} team_get_config mask 0")
+            r, t = ish.ishmem_team_split_strided(ish.ISHMEM_TEAM_WORLD, 0, 1, npes)
+            if r or ish.lib().ishmemi_c_team_set_config(t, 1, 7) or ish.ishmem_team_get_config(t) != (0, 7):
+                fails.append(f"pe{pe} team config round trip {ish.last_error()}")
+            ish.ishmem_team_destroy(t)
+            if ish.ishmem_team_get_config(t)[0] == 0:
+                fails.append(f"pe{pe} team_get_config of a destroyed team succeeded")
+
+        if "bcast" in scenarios:
+            # Host broadcast (ishmem_<TN>_broadcast / broadcastmem, src/ishmem.h:761-813): every
+            # root, symmetric / device / pinned-host dest, the root's source in host memory
+            # (staged) while the others pass a heap address, odd byte counts, 0 bytes (a team
+            # sync), a strided team.  Then the blocking fcollect / scan with members passing
+            # different kinds of source (they agree on the staged path first), and a member whose
+            # dest is not device-writable: every member fails, none hangs.
+            n = 70_001
+            src_b, dst_b = ish.ishmem_malloc(4 * n + 64), ish.ishmem_malloc(4 * n + 64)
+            ddev = hip.malloc(4 * n)
+            hdst = hip.host_malloc(4 * n)
+            hview = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_int32 * n).from_address(hdst))
+            for root in range(npes):
+                vals = [oracle.fill_random(DT["int32"], 0xB0 + j, n) for j in range(npes)]
+                hip.upload(src_b, vals[pe])
+                for kind, dst in (("heap", dst_b), ("device", ddev), ("pinned", hdst)):
+                    hip.memset(dst, 0, 4 * n)
+                    if ish.ishmem_int32_broadcast(dst, src_b, n, root):
+                        fails.append(f"pe{pe} bcast root {root} {kind}: {ish.last_error()}")
+                        continue
+                    got = hview.copy() if kind == "pinned" else hip.download(dst, n, np.int32)
+                    if not np.array_equal(got, vals[root]):
+                        fails.append(f"pe{pe} bcast root {root} into {kind} memory wrong")
+                hs = np.ascontiguousarray(vals[pe])
+                if ish.ishmem_int32_broadcast(dst_b, hs.ctypes.data if pe == root else src_b, n, root) or \
+                        not np.array_equal(hip.download(dst_b, n, np.int32), vals[root]):
+                    fails.append(f"pe{pe} bcast root {root} from host memory wrong {ish.last_error()}")
+            for nb in (1, 7, 1001):
+                hip.upload(src_b + 3, np.arange(nb, dtype=np.uint8) + np.uint8(pe))
+                if ish.ishmem_broadcastmem(dst_b + 1, src_b + 3, nb, npes - 1) or not np.array_equal(
+                        hip.download(dst_b + 1, nb, np.uint8), np.arange(nb, dtype=np.uint8) + np.uint8(npes - 1)):
+                    fails.append(f"pe{pe} broadcastmem {nb} B wrong {ish.last_error()}")
+            if ish.ishmem_broadcastmem(dst_b, src_b, 0, 0):
+                fails.append(f"pe{pe} broadcastmem 0 B {ish.last_error()}")
+            r, team = ish.ishmem_team_split_strided(ish.ISHMEM_TEAM_WORLD, 0, 2, (npes + 1) // 2)
+            if team != ish.ISHMEM_TEAM_INVALID:
+                members = list(range(0, npes, 2))
+                root = len(members) - 1
+                hip.upload(src_b, np.full(100, 1000 + pe, np.int64))
+                if ish.ishmem_long_broadcast(team, dst_b, src_b, 100, root) or not np.all(
+                        hip.download(dst_b, 100, np.int64) == 1000 + members[root]):
+                    fails.append(f"pe{pe} team broadcast wrong {ish.last_error()}")
+                ish.ishmem_team_destroy(team)
+            # fcollect / scan with mixed source kinds (PE 0's source in host memory).
+            m = 50_000
+            vals = [oracle.fill_random(DT["int32"], 0xC0 + j, m) for j in range(npes)]
+            hip.upload(src_b, vals[pe])
+            hsrc = np.ascontiguousarray(vals[pe])
+            fdst = ish.ishmem_malloc(4 * m * npes)
+            if ish.ishmem_int32_fcollect(fdst, hsrc.ctypes.data if pe == 0 else src_b, m) or not np.array_equal(
+                    hip.download(fdst, m * npes, np.int32), np.concatenate(vals)):
+                fails.append(f"pe{pe} fcollect with mixed source kinds wrong {ish.last_error()}")
+            for inc in (True, False):
+                hip.memset(dst_b, 0, 4 * m)
+                if ish.scan("int32", inc, dst_b, hsrc.ctypes.data if pe == 0 else src_b, m) or not _bits_equal(
+                        hip.download(dst_b, m, np.int32), oracle.scan_fold(DT["int32"], vals, pe, inc)):
+                    fails.append(f"pe{pe} scan inc={inc} with mixed source kinds wrong {ish.last_error()}")
+            pageable = np.zeros(m * npes, np.int32)
+            bad_dst = pageable.ctypes.data if pe == npes - 1 else fdst
+            t0 = time.perf_counter()
+            if ish.ishmem_int32_fcollect(bad_dst, src_b, m) == 0:
+                fails.append(f"pe{pe} fcollect with a member's pageable dest succeeded")
+            if ish.ishmem_int32_collect(bad_dst, src_b, m) == 0:
+                fails.append(f"pe{pe} collect with a member's pageable dest succeeded")
+            if time.perf_counter() - t0 > 5.0:
+                fails.append(f"pe{pe} argument failure took {time.perf_counter() - t0:.1f} s (a member waited)")
+            # the team still works afterwards (nothing was launched by the failed calls)
+            if ish.ishmem_int32_fcollect(fdst, src_b, m) or not np.array_equal(
+                    hip.download(fdst, m * npes, np.int32), np.concatenate(vals)):
+                fails.append(f"pe{pe} fcollect after the refused call wrong {ish.last_error()}")
+            del hview
+            hip.host_free(hdst)
+            hip.free(ddev)
+            for b_ in (fdst, dst_b, src_b):
+                ish.ishmem_free(b_)
 
         if "golden" in scenarios:
             z = np.load(GOLDEN / f"golden_np{npes}.npz") if (GOLDEN / f"golden_np{npes}.npz").exists() else None

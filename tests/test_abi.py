@@ -131,3 +131,87 @@ def test_c_header_is_plain_c(tmp_path):
     src.write_text('#include "ishmem_capi.h"\nint main(void){return ishmemi_c_n_pes() == -1 ? 0 : 1;}\n')
     subprocess.run([gcc, "-std=c99", "-Wall", "-Werror", f"-I{INCLUDE}", "-c", str(src), "-o",
                     str(tmp_path / "t.o")], check=True)
+
+
+def test_setup_surface_of_the_reference_header_compiles(tmp_path):
+    # src/ishmem.h:17-26 (version, thread levels), :44-45 (init_thread / query_thread), :57-58
+    # (info_get_*), :63-67 / :78 (team config), :761-813 (broadcast) — with host g++, no GPU.
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    src = tmp_path / "t.cpp"
+    src.write_text(r'''
+#include <ishmem.h>
+#include <ishmemx.h>
+#include <cstdio>
+#include <cstring>
+int main() {
+    int major = 0, minor = 0, provided = -1;
+    char name[ISHMEM_MAX_NAME_LEN];
+    ishmem_info_get_version(&major, &minor);
+    ishmem_info_get_name(name);
+    ishmem_query_thread(&provided);
+    ishmem_team_config_t cfg = {3};
+    ishmem_team_config_t *config = NULL;
+    ishmem_team_t t = ISHMEM_TEAM_INVALID;
+    int r1 = ishmem_team_get_config(ISHMEM_TEAM_WORLD, ISHMEM_TEAM_NUM_CONTEXTS, &cfg);  // not initialised
+    int r2 = ishmem_team_split_strided(ISHMEM_TEAM_WORLD, 0, 2, 1, config, 0, &t);
+    int r3 = ishmem_int_broadcast((int *) nullptr, nullptr, 0, 0);
+    int r4 = ishmem_broadcastmem(ISHMEM_TEAM_WORLD, nullptr, nullptr, 0, 0);
+    std::printf("%d %d %d %s %d %d %d %d %d\n", major, minor, provided, std::strlen(name) > 0 ? "named" : "-",
+                r1 != 0, r2 != 0, r3 != 0, r4 != 0, ISHMEM_THREAD_MULTIPLE);
+    return 0;
+}
+''')
+    exe = tmp_path / "t"
+    subprocess.run([gxx, "-std=c++17", f"-I{INCLUDE}", str(src), "-o", str(exe),
+                    f"-L{_lib.LIB_PATH.parent}", f"-Wl,-rpath,{_lib.LIB_PATH.parent}", "-lishmem_amd"],
+                   check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["1", "5", "3", "named", "1", "1", "1", "1", "3"]
+
+
+def test_device_api_compiles_without_a_context_argument(tmp_path):
+    # The reference's device calls, verbatim, inside HIP kernels (hipcc, gfx950; compile only).
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not Path(hipcc).exists():
+        pytest.skip("no hipcc")
+    src = tmp_path / "t.hip"
+    src.write_text(r'''
+#include <hip/hip_cooperative_groups.h>
+#include <ishmem.h>
+#include <ishmemx.h>
+namespace cg = cooperative_groups;
+__global__ void k(int *dst_sum, int *reduce_src, int *dst, int *src, ishmem_team_t team, double *fd, double *fs) {
+    auto grp = cg::this_thread_block();
+    auto wave = cg::tiled_partition<64>(grp);
+    int my_dev_pe = ishmem_my_pe(), my_dev_npes = ishmem_n_pes();
+    if (grp.thread_rank() == 0) ishmem_barrier_all();
+    ishmemx_barrier_all_work_group(grp);
+    ishmemx_sync_all_work_group(grp);
+    ishmemx_team_sync_work_group(team, grp);
+    if (grp.thread_rank() == 0) ishmem_int_sum_reduce(dst_sum, reduce_src, 1);
+    ishmemx_int_sum_reduce_work_group(dst_sum, reduce_src, 1, grp);
+    ishmemx_int_sum_reduce_work_group(team, dst_sum, reduce_src, 1, grp);
+    ishmemx_double_prod_reduce_work_group(fd, fs, 8, wave);
+    ishmemx_sum_reduce_work_group(fd, fs, 8, grp);          // generic
+    ishmemx_broadcastmem_work_group(dst, src, 4, 0, grp);
+    ishmemx_int_fcollect_work_group(dst, src, 1, grp);
+    ishmemx_int_sum_inscan_work_group(team, dst, src, 1, grp);
+    if (grp.thread_rank() == 0) {
+        ishmem_int_sum_reduce(team, dst_sum, reduce_src, 1);
+        ishmem_int_broadcast(team, dst, src, 1, 0);
+        ishmem_team_sync(ISHMEM_TEAM_WORLD);
+        ishmem_sync_all();
+        int t = ishmem_team_my_pe(team) + ishmem_team_n_pes(team) + ishmem_team_translate_pe(team, 0, ISHMEM_TEAM_WORLD);
+        void *p = ishmem_ptr(dst, (my_dev_pe + 1) % my_dev_npes);
+        int mj, mn;
+        ishmem_info_get_version(&mj, &mn);
+        if (!p || t < 0) ishmemx_print("unexpected\n", ishmemx_print_msg_type_t::ERROR);
+    }
+}
+int main() { return 0; }
+''')
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-std=c++20", f"-I{INCLUDE}", "-c", str(src), "-o",
+                    str(tmp_path / "t.o")], check=True)

@@ -208,3 +208,19 @@ def test_concurrent_collectives_of_different_teams_on_different_streams(npes):
     # x-team and y-team reduces of a 2-D split plus a WORLD reduce in flight together on three
     # streams (TP / DP groups), no synchronisation between them; full grids per PE.
     run_pes(npes, ["concurrent"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "1G"}, timeout=300)
+
+
+@pytest.mark.parametrize("npes", [2, 3, 4])
+def test_broadcast_setup_surface_and_agreed_paths(npes):
+    # Host broadcast (every root, dest kinds, staged root source, teams), the setup surface
+    # (threading, info, team config), fcollect / scan with mixed source kinds and a refused call
+    # that fails on every member without a launch.
+    run_pes(npes, ["setup", "bcast"], env={"ISHMEM_STAGING_SIZE": "4M"})
+
+
+@pytest.mark.parametrize("forced", [False, True])
+def test_coarse_grained_flags_across_devices_refused_at_init(forced):
+    env = {"ISHMEM_TEST_FLAGS_UNAVAILABLE": 1, "ISHMEM_TEST_PCI_BUS": ["fake-bus-0", "fake-bus-1"]}
+    if forced:
+        env["ISHMEM_FLAGS_KIND"] = 2
+    run_pes(2, ["refuse"], env=env, timeout=120)
