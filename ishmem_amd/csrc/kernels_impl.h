@@ -183,7 +183,11 @@ __device__ __forceinline__ void kernel_epoch_done(const A &a, uint32_t ep)
                  gridDim.x - 1;
     __syncthreads();
     if (s_last && threadIdx.x < 64) {
-        if (threadIdx.x == 0) __hip_atomic_store(a.ep_ctr + kEpDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // Every launch word back to zero, the failure word included (a timed-out team sync must
+        // not make the team's next collective drain at once), as launch_finish does.
+        if (threadIdx.x == 0)
+            for (int k = kEpDone; k < kEpWords; ++k)
+                __hip_atomic_store(a.ep_ctr + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         publish_epoch_wave(a, ep);
     }
 }
