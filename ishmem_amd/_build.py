@@ -44,17 +44,23 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in _deps())
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, defines: list[str] | None = None,
+          out: Path | None = None) -> Path:
+    """Build the library (or, with `defines` / `out`, an A/B variant of it at `out`, objects
+    under build/native/<out stem>; the product library is never replaced by a variant)."""
+    lib = LIB if out is None else Path(out)
+    if out is None and not force and not needs_build():
         return LIB
     hipcc = _hipcc()
-    BUILD.mkdir(parents=True, exist_ok=True)
+    bdir = BUILD if out is None else BUILD / lib.stem
+    bdir.mkdir(parents=True, exist_ok=True)
+    lib.parent.mkdir(parents=True, exist_ok=True)
     common = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
-              "-Wall", "-Wno-unused-function"]
+              "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in (defines or [])]]
     objs = []
     procs = []
     for src, stem, extra in SOURCES:
-        obj = BUILD / (stem + ".o")
+        obj = bdir / (stem + ".o")
         objs.append(obj)
         cmd = [hipcc, *common, *extra, "-c", str(CSRC / src), "-o", str(obj)]
         if verbose:
@@ -64,14 +70,18 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         out, _ = p.communicate()
         if p.returncode != 0:
             raise RuntimeError(f"hipcc failed: {' '.join(cmd)}\n{out.decode(errors='replace')}")
-    tmp = LIB.with_suffix(".so.tmp")
+    tmp = lib.with_suffix(".so.tmp")
     cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout.decode(errors='replace')}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    # python -m ishmem_amd._build [--force] [--define NAME=V ... --out PATH]  (A/B variants)
+    args = sys.argv[1:]
+    defs = [args[i + 1] for i, a in enumerate(args) if a == "--define"]
+    outp = args[args.index("--out") + 1] if "--out" in args else None
+    print(build(force="--force" in args, verbose=True, defines=defs, out=Path(outp) if outp else None))

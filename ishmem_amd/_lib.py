@@ -6,9 +6,13 @@ loudly (there is no Python / CPU fallback).
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libishmem_amd.so"
+# A/B measurements only: ISHMEM_AMD_LIB names a variant build of the same library
+# (python -m ishmem_amd._build --define ... --out build/ab/<name>.so); never set for results.
+_VARIANT = os.environ.get("ISHMEM_AMD_LIB")
 
 # (name, restype, argtypes) for every symbol declared in include/ishmem_capi.h.
 _vp, _i, _sz, _ll, _u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_longlong, ctypes.c_uint64
@@ -77,6 +81,14 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    if _VARIANT:
+        lib = ctypes.CDLL(str(Path(_VARIANT).resolve()), mode=ctypes.RTLD_GLOBAL)
+        for name, res, args in PROTOTYPES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
     if build_if_missing:
         from . import _build
         if _build.needs_build():

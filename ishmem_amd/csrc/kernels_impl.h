@@ -461,7 +461,11 @@ __device__ __forceinline__ void rs_tile(const ReduceArgs &a, uint64_t t0, uint64
     // Items per thread per step: P * H = 8 loads staged in registers for P in {2, 4, 8}
     // (MI355X_MICROARCH.md: keep >= 8 loads per lane outstanding on streamed hand-offs; more
     // pushed the kernel past 128 VGPRs, i.e. below 4 workgroups per CU).
+#if ISHMEMI_AB_OCC4  // A/B variant: 4 workgroups per CU, half the loads staged
+    constexpr int H = sizeof(T) >= 4 ? (P <= 2 ? 2 : 1) : 1;
+#else
     constexpr int H = sizeof(T) >= 4 ? (P <= 2 ? 4 : P == 4 ? 2 : 1) : 1;
+#endif
     const uint32_t tid = threadIdx.x;
     // Items left in this tile (wave-uniform, <= kTile): 32-bit per-lane bounds checks.
     const uint32_t lim = (uint32_t) min<uint64_t>(ce - t0, kTile);
@@ -709,8 +713,13 @@ __device__ __forceinline__ void rs_segment(const ReduceArgs &a, uint32_t ep, uin
     }
 }
 
+#if ISHMEMI_AB_OCC4
+constexpr int kArOcc = 4, kAgTiles = 1;
+#else
+constexpr int kArOcc = 3, kAgTiles = 2;  // workgroups per CU; all-gather tiles per step
+#endif
 template <typename T, int OP, bool VEC, int P>
-__global__ __launch_bounds__(kBlock, sizeof(T) == 1 ? 2 : 3) __attribute__((flatten)) void allreduce_kernel(ReduceArgs a)
+__global__ __launch_bounds__(kBlock, sizeof(T) == 1 ? 2 : kArOcc) __attribute__((flatten)) void allreduce_kernel(ReduceArgs a)
 {
     using Item = std::conditional_t<VEC, Vec<T>, T>;
     constexpr uint64_t IB = sizeof(Item);
@@ -806,10 +815,10 @@ __global__ __launch_bounds__(kBlock, sizeof(T) == 1 ? 2 : 3) __attribute__((flat
                 have_item = false;
                 // The segment's tiles, two per step: 8 loads per lane in flight.
                 const uint64_t ss = js + (uint64_t) s * seg, se = min(ss + seg, je);
-                for (uint64_t t = ss; t < se; t += 2 * kTile) {
+                for (uint64_t t = ss; t < se; t += kAgTiles * kTile) {
                     // Two tiles in one descriptor window (offsets < 32 KiB): 8 loads per lane.
-                    constexpr int U = 2 * kUnroll;
-                    const uint32_t lim = (uint32_t) min<uint64_t>(se - t, 2 * kTile);
+                    constexpr int U = kAgTiles * kUnroll;
+                    const uint32_t lim = (uint32_t) min<uint64_t>(se - t, kAgTiles * kTile);
                     const __amdgpu_buffer_rsrc_t r = make_rsrc(uniform_ptr(a.dstp[j] + head_bytes + t * IB));
                     Item x[U];
 #pragma unroll
