@@ -42,6 +42,9 @@ namespace {
 // sc0|sc1 cache policy on gfx950 buffer instructions = system-coherent access.
 constexpr int kSysCoherent = 17;
 constexpr uint64_t kTile = (uint64_t) kBlock * kUnroll;  // items per tile
+#ifndef ISHMEMI_AR_OCC
+#define ISHMEMI_AR_OCC 4  // multi-PE kernel: workgroups per CU (see allreduce_kernel)
+#endif
 
 template <typename T>
 struct alignas(16) Vec {
@@ -461,7 +464,7 @@ __device__ __forceinline__ void rs_tile(const ReduceArgs &a, uint64_t t0, uint64
     // Items per thread per step: P * H = 8 loads staged in registers for P in {2, 4, 8}
     // (MI355X_MICROARCH.md: keep >= 8 loads per lane outstanding on streamed hand-offs; more
     // pushed the kernel past 128 VGPRs, i.e. below 4 workgroups per CU).
-#if ISHMEMI_AB_OCC4  // A/B variant: 4 workgroups per CU, half the loads staged
+#if ISHMEMI_AR_OCC >= 4
     constexpr int H = sizeof(T) >= 4 ? (P <= 2 ? 2 : 1) : 1;
 #else
     constexpr int H = sizeof(T) >= 4 ? (P <= 2 ? 4 : P == 4 ? 2 : 1) : 1;
@@ -713,10 +716,14 @@ __device__ __forceinline__ void rs_segment(const ReduceArgs &a, uint32_t ep, uin
     }
 }
 
-#if ISHMEMI_AB_OCC4
+// Workgroups per CU of the multi-PE kernel and all-gather tiles per step.  Round 3's A/B
+// (profiles/r03/ab_occ/): 4 per CU with 4 loads per lane staged against round 2's
+// 3 per CU with 8 — 8 PEs on one GPU 3.90 vs 4.55 ms per 1 GiB call, 2 PEs within noise
+// (1.05 vs 1.07 ms).  ISHMEMI_AR_OCC=3 builds the round-2 shape (A/B variants only).
+#if ISHMEMI_AR_OCC >= 4
 constexpr int kArOcc = 4, kAgTiles = 1;
 #else
-constexpr int kArOcc = 3, kAgTiles = 2;  // workgroups per CU; all-gather tiles per step
+constexpr int kArOcc = 3, kAgTiles = 2;
 #endif
 template <typename T, int OP, bool VEC, int P>
 __global__ __launch_bounds__(kBlock, sizeof(T) == 1 ? 2 : kArOcc) __attribute__((flatten)) void allreduce_kernel(ReduceArgs a)
