@@ -476,6 +476,38 @@ def cpu_baseline_leg(ish, hip, src, dst, n, B, world, rank, dist, key) -> tuple[
     return cpu, extra
 
 
+def pcie_probe(hip, hs: int, hd: int, B: int, dist) -> dict:
+    """hipMemcpyAsync of B bytes pinned host -> HBM and HBM -> pinned host on their own streams:
+    each direction alone, then both at once (GB/s, max time over ranks), 2 reps each."""
+    d1, d2 = hip.malloc(B), hip.malloc(B)
+    s1, s2 = hip.stream_create(), hip.stream_create()
+    try:
+        def timed(jobs, reps=2):
+            for dst, src, st in jobs:  # warm-up
+                hip.memcpy_async(dst, src, B, st)
+            for _, _, st in jobs:
+                hip.stream_synchronize(st)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                for dst, src, st in jobs:
+                    hip.memcpy_async(dst, src, B, st)
+            for _, _, st in jobs:
+                hip.stream_synchronize(st)
+            return max_over_ranks(dist, [(time.perf_counter() - t0) / reps])[0]
+        h2d = B / timed([(d1, hs, s1)]) / 1e9
+        d2h = B / timed([(hd, d2, s2)]) / 1e9
+        both = B / timed([(d1, hs, s1), (hd, d2, s2)]) / 1e9  # each direction's rate while both run
+        return {"h2d_GBps": round(h2d, 2), "d2h_GBps": round(d2h, 2), "concurrent_min_GBps": round(both, 2),
+                "bytes": B, "note": "hipMemcpyAsync, pinned host <-> HBM; concurrent = H2D and D2H on two streams"}
+    except Exception as ex:
+        return {"error": str(ex)}
+    finally:
+        hip.stream_destroy(s1)
+        hip.stream_destroy(s2)
+        hip.free(d1)
+        hip.free(d2)
+
+
 def e2e_leg(ish, hip, n, B, world, rank, dist, stream, barrier, steps, pinned: bool) -> dict:
     """Host-memory end-to-end rate: ishmemx_float_sum_reduce_on_stream on host source / dest (the
     reference's host path is reduce_impl.h:186-228, :301-315); every word of dest checked."""
@@ -519,6 +551,13 @@ def e2e_leg(ish, hip, n, B, world, rank, dist, stream, barrier, steps, pinned: b
                "checked": bad == 0, "words_checked": n, "mode": "every word, every rank",
                "buffers": "pinned host (hipHostMalloc)" if pinned else "pageable host (malloc'd numpy)",
                "pipeline": "H2D | reduce | D2H over 2 staging slots"}
+        if pinned:
+            # What bounds the leg: plain DMA copies of the same B between these pinned buffers and
+            # HBM, each direction alone and both at once (the pipeline moves B each way per step).
+            out["pcie_probe"] = pcie_probe(hip, hs, hd, B, dist)
+            both = out["pcie_probe"].get("concurrent_min_GBps")
+            if both:
+                out["frac_of_concurrent_dma"] = (B / (te / k) / 1e9) / both
         del xs, xd
         if pinned:
             hip.host_free(hs)
@@ -693,9 +732,11 @@ def main() -> int:
         try:
             probe = xgmi_probe(ish, hip, src, dst, B, world, rank, dist, stream, barrier)
             extra["xgmi_probe"] = probe
-            # Same accounting as roof["achieved"], against the measured all-peer ingress.
-            roof["peak_measured"] = max(probe["pullall"]["ingress_GBps"], probe["pullall_sc"]["ingress_GBps"])
-            roof["frac_measured"] = roof["achieved"] / roof["peak_measured"]
+            # Same accounting as roof["achieved"] (per-PE ingress), against the measured all-peer
+            # ingress; only meaningful when the bound is xGMI (one PE per GPU).
+            if roof["bound"] == "xgmi":
+                roof["peak_measured"] = max(probe["pullall"]["ingress_GBps"], probe["pullall_sc"]["ingress_GBps"])
+                roof["frac_measured"] = roof["achieved"] / roof["peak_measured"]
         except Exception as ex:
             extra["xgmi_probe"] = {"error": str(ex)}
 

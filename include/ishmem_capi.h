@@ -127,6 +127,9 @@ int ishmemi_c_team_set_config(int team, long config_mask, int num_contexts);
 int ishmemi_c_barrier_all(void);
 int ishmemi_c_sync_all(void);
 int ishmemi_c_team_sync(int team);
+/* The team barrier enqueued on `stream` (ishmemx_team_sync_on_queue / sync_all_on_queue /
+ * barrier_all_on_queue, src/ishmemx.h:2228-2235); *ret as for ishmemi_c_reduce_on_stream. */
+int ishmemi_c_team_sync_on_stream(int team, int *ret, void *stream);
 /* Recovery after a device-side timeout (no reference counterpart: the reference aborts the job,
  * src/proxy.cpp:79-84).  Collective over ALL PEs, called with no collective in flight: the PEs
  * agree on the newest epoch of every team over the bootstrap, so later collectives of a team whose
@@ -206,6 +209,11 @@ int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *s
  * (ishmem_<TN>_broadcast / ishmem_broadcastmem, src/ishmem.h:761-813, broadcast_impl.h's pull
  * variant).  `root` is the root's index in the team.  Sources outside the heap are staged. */
 int ishmemi_c_broadcast(int team, void *dest, const void *source, size_t nbytes, int root);
+/* broadcast enqueued on `stream` (ishmemx_<TN>_broadcast_on_queue, src/ishmemx.h:846-954): the
+ * source must be symmetric-heap memory (the root's is found at the same offset), dest
+ * device-writable on every member.  *ret as for ishmemi_c_reduce_on_stream. */
+int ishmemi_c_broadcast_on_stream(int team, void *dest, const void *source, size_t nbytes, int root,
+                                  int *ret, void *stream);
 int ishmemi_c_scan_on_stream(int team, int dtype, int inclusive, void *dest, const void *source,
                              size_t nelems, int *ret, void *stream);
 /* The `deps` / returned-event plumbing of every _on_queue form (fcollect, collect, inscan, exscan;

@@ -247,6 +247,58 @@ ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_COLL_ON_STREAM, _, _)
 
 ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_COLL_ON_STREAM_EV, _, _)
 
+/* broadcast / team barrier on a stream (src/ishmemx.h:846-954, :2228-2235). */
+inline int ishmemx_broadcastmem_on_stream(ishmem_team_t team, void *dest, const void *source, size_t nbytes,
+                                          int root, int *ret, hipStream_t stream)
+{
+    return ishmemi_c_broadcast_on_stream(team, dest, source, nbytes, root, ret, (void *) stream);
+}
+inline int ishmemx_broadcastmem_on_stream(void *dest, const void *source, size_t nbytes, int root, int *ret,
+                                          hipStream_t stream)
+{
+    return ishmemi_c_broadcast_on_stream(ISHMEM_TEAM_WORLD, dest, source, nbytes, root, ret, (void *) stream);
+}
+template <typename T>
+inline int ishmemx_broadcast_on_stream(ishmem_team_t team, T *dest, const T *source, size_t nelems, int root,
+                                       int *ret, hipStream_t stream)
+{
+    return ishmemi_c_broadcast_on_stream(team, (void *) dest, (const void *) source, nelems * sizeof(T), root, ret,
+                                         (void *) stream);
+}
+template <typename T>
+inline int ishmemx_broadcast_on_stream(T *dest, const T *source, size_t nelems, int root, int *ret,
+                                       hipStream_t stream)
+{
+    return ishmemx_broadcast_on_stream(ISHMEM_TEAM_WORLD, dest, source, nelems, root, ret, stream);
+}
+#define ISHMEMI_CXX_BCAST_ON_STREAM(TYPENAME, TYPE, UNUSED1, UNUSED2)                               \
+    inline int ishmemx_##TYPENAME##_broadcast_on_stream(ishmem_team_t team, TYPE *dest,             \
+                                                        const TYPE *source, size_t nelems, int root, \
+                                                        int *ret, hipStream_t stream)              \
+    {                                                                                              \
+        return ishmemx_broadcast_on_stream(team, dest, source, nelems, root, ret, stream);         \
+    }                                                                                              \
+    inline int ishmemx_##TYPENAME##_broadcast_on_stream(TYPE *dest, const TYPE *source,             \
+                                                        size_t nelems, int root, int *ret,         \
+                                                        hipStream_t stream)                        \
+    {                                                                                              \
+        return ishmemx_broadcast_on_stream(dest, source, nelems, root, ret, stream);               \
+    }
+ISHMEMI_CXX_ARITH_TYPES(ISHMEMI_CXX_BCAST_ON_STREAM, _, _)
+inline int ishmemx_team_sync_on_stream(ishmem_team_t team, int *ret, hipStream_t stream)
+{
+    return ishmemi_c_team_sync_on_stream(team, ret, (void *) stream);
+}
+inline int ishmemx_sync_all_on_stream(hipStream_t stream)
+{
+    return ishmemi_c_team_sync_on_stream(ISHMEM_TEAM_WORLD, nullptr, (void *) stream);
+}
+/* barrier_all = quiet + sync_all; stream order already completes the stream's earlier work. */
+inline int ishmemx_barrier_all_on_stream(hipStream_t stream)
+{
+    return ishmemi_c_team_sync_on_stream(ISHMEM_TEAM_WORLD, nullptr, (void *) stream);
+}
+
 /* Explicit-identity init (the role of ishmemx_init_attr, src/ishmemx.h:21-37). */
 inline int ishmemx_init_pe(int pe, int npes, int device, const char *bootstrap_key)
 {

@@ -319,6 +319,17 @@ def ishmem_broadcastmem(*args) -> int:
     return _L.ishmemi_c_broadcast(team, dest, source, n, root)
 
 
+def broadcast_on_stream(dest: int, source: int, nbytes: int, root: int, ret: int | None, stream: int,
+                        team: int = ISHMEM_TEAM_WORLD) -> int:
+    """ishmemx_broadcastmem_on_queue analogue: symmetric source, the root's bytes into every dest."""
+    return _L.ishmemi_c_broadcast_on_stream(team, dest, source, nbytes, root, ret or None, stream or None)
+
+
+def team_sync_on_stream(team: int, ret: int | None, stream: int) -> int:
+    """ishmemx_team_sync_on_queue analogue (src/ishmemx.h:2235)."""
+    return _L.ishmemi_c_team_sync_on_stream(team, ret or None, stream or None)
+
+
 def scan(dtype: str, inclusive: bool, dest: int, source: int, nelems: int,
          team: int = ISHMEM_TEAM_WORLD) -> int:
     return _L.ishmemi_c_scan(team, DTYPES[dtype], 1 if inclusive else 0, dest, source, nelems)

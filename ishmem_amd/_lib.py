@@ -43,6 +43,7 @@ PROTOTYPES = [
     ("ishmemi_c_barrier_all", _i, []),
     ("ishmemi_c_sync_all", _i, []),
     ("ishmemi_c_team_sync", _i, [_i]),
+    ("ishmemi_c_team_sync_on_stream", _i, [_i, _vp, _vp]),
     ("ishmemi_c_resync", _i, []),
     ("ishmemi_c_reduce", _i, [_i, _i, _i, _vp, _vp, _sz]),
     ("ishmemi_c_reduce_on_stream", _i, [_i, _i, _i, _vp, _vp, _sz, _vp, _vp]),
@@ -60,6 +61,7 @@ PROTOTYPES = [
     ("ishmemi_c_scan", _i, [_i, _i, _i, _vp, _vp, _sz]),
     ("ishmemi_c_scan_on_stream", _i, [_i, _i, _i, _vp, _vp, _sz, _vp, _vp]),
     ("ishmemi_c_broadcast", _i, [_i, _vp, _vp, _sz, _i]),
+    ("ishmemi_c_broadcast_on_stream", _i, [_i, _vp, _vp, _sz, _i, _vp, _vp]),
     ("ishmemi_c_device_ctx", _vp, []),
     ("ishmemi_c_register_device_ctx_slot", _i, [_vp]),
     ("ishmemi_c_last_error", ctypes.c_char_p, []),

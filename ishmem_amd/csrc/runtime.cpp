@@ -1566,6 +1566,19 @@ int ishmemi_c_team_sync(int team)
 
 int ishmemi_c_sync_all(void) { return ishmemi_c_team_sync(ISHMEMI_C_TEAM_WORLD); }
 
+int ishmemi_c_team_sync_on_stream(int team, int *ret, void *stream)
+{
+    // ishmemx_team_sync_on_queue / sync_all_on_queue / barrier_all_on_queue (src/ishmemx.h:2228-2235):
+    // the team barrier kernel enqueued on `stream` (stream order completes everything before it).
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!member_call(s, team)) return fail("team_sync_on_stream: not initialized, invalid team or caller not a member");
+    hipStream_t st = (hipStream_t) stream;
+    if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
+    if (team_sync_locked(s, team, st, ret)) return 1;
+    return mark_stream(s, st);
+}
+
 int ishmemi_c_barrier_all(void)
 {
     // ishmem_barrier_all = quiet + sync_all: complete all outstanding device work first.
@@ -1822,6 +1835,42 @@ int ishmemi_c_scan(int team, int dtype, int inclusive, void *dest, const void *s
     if (td) heap_free(s, td);
     if (ts) heap_free(s, ts);
     return rc;
+}
+
+int ishmemi_c_broadcast_on_stream(int team, void *dest, const void *source, size_t nbytes, int root,
+                                  int *ret, void *stream)
+{
+    // ishmemx_<TN>_broadcast_on_queue (src/ishmemx.h:846-954): nothing can be exchanged on the host
+    // here, so the source is a symmetric address (the root's is found at the same offset of its
+    // heap, as the reference requires of symmetric objects) and every member's dest must be
+    // device-writable.
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!member_call(s, team)) return fail("broadcast_on_stream: not initialized, invalid team or caller not a member");
+    const Team &t = s.teams[team];
+    if (root < 0 || root >= t.size) return fail("broadcast_on_stream: root is not a team index");
+    hipStream_t st = (hipStream_t) stream;
+    if (ret) HIP_TRY(hipMemsetAsync(ret, 0, sizeof(int), st));
+    if (t.size == 1) {
+        if (nbytes && dest != source) {
+            if (device_writable(s, dest) && classify(s, source) != Kind::Host) {
+                if (launch_copy(dest, source, nbytes, st)) return 1;
+            } else {
+                HIP_TRY(hipMemcpyAsync(dest, source, nbytes, hipMemcpyDefault, st));
+            }
+        }
+        return mark_stream(s, st);
+    }
+    if (nbytes == 0) return team_sync_locked(s, team, st, ret) || mark_stream(s, st);
+    if (!in_heap(s, source)) return fail("broadcast_on_stream: source must be symmetric-heap memory");
+    if (!device_writable(s, dest)) return fail("broadcast_on_stream: dest must be heap, device or pinned host memory");
+    uint64_t counts[kMaxPes] = {}, zero[kMaxPes] = {};
+    counts[root] = nbytes;
+    const char *srcs[kMaxPes];
+    const char *rsrc = translate(s, source, t.start + root * t.stride);
+    for (int j = 0; j < t.size; ++j) srcs[j] = rsrc;
+    if (collect_launch(s, team, dest, nullptr, counts, ret, st, zero, srcs)) return 1;
+    return mark_stream(s, st);
 }
 
 int ishmemi_c_broadcast(int team, void *dest, const void *source, size_t nbytes, int root)

@@ -226,6 +226,28 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             if ish.ishmem_int32_fcollect(fdst, src_b, m) or not np.array_equal(
                     hip.download(fdst, m * npes, np.int32), np.concatenate(vals)):
                 fails.append(f"pe{pe} fcollect after the refused call wrong {ish.last_error()}")
+            # On a stream (ishmemx_*_broadcast_on_queue / team_sync_on_queue): a reduce, then a
+            # broadcast of one member's result block, then a team barrier, chained with no host
+            # synchronisation; *ret stays 0.
+            st_b = hip.stream_create()
+            ret_b = ish.ishmem_malloc(4)
+            hip.memset(ret_b, 0x7F, 4)
+            vals = [oracle.fill_random(DT["int32"], 0xD0 + j, m) for j in range(npes)]
+            hip.upload(src_b, vals[pe])
+            ish.ishmem_barrier_all()
+            root = npes // 2
+            rc = [ish.reduce_on_stream("max", "int32", fdst, src_b, m, ret_b, st_b),
+                  ish.broadcast_on_stream(dst_b, src_b, 4 * 1000, root, ret_b, st_b),
+                  ish.team_sync_on_stream(ish.ISHMEM_TEAM_WORLD, ret_b, st_b)]
+            hip.stream_synchronize(st_b)
+            if any(rc) or int(hip.download(ret_b, 1, np.int32)[0]) != 0:
+                fails.append(f"pe{pe} on-stream broadcast chain rc={rc} {ish.last_error()}")
+            else:
+                check("on-stream max before broadcast", OPS["max"], DT["int32"], vals, hip.download(fdst, m, np.int32))
+                if not np.array_equal(hip.download(dst_b, 1000, np.int32), vals[root][:1000]):
+                    fails.append(f"pe{pe} on-stream broadcast wrong")
+            hip.stream_destroy(st_b)
+            ish.ishmem_free(ret_b)
             del hview
             hip.host_free(hdst)
             hip.free(ddev)
