@@ -553,10 +553,16 @@ struct CallPins {
         if (!p || bytes < kPinMinBytes || !pageable_host(p)) return;
         for (void *q : pinned)
             if (q == p) return;  // in place: one registration
-        if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
+        const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterDefault);
+        if (e != hipSuccess) {
             (void) hipGetLastError();
+            if (getenv("ISHMEM_DEBUG") && atoi(getenv("ISHMEM_DEBUG")) > 0)
+                fprintf(stderr, "[ishmem_amd] hipHostRegister(%p, %zu): %s (synchronous copies)\n", p, bytes,
+                        hipGetErrorString(e));
             return;
         }
+        if (getenv("ISHMEM_DEBUG") && atoi(getenv("ISHMEM_DEBUG")) > 1)
+            fprintf(stderr, "[ishmem_amd] page-locked %p, %zu bytes for the call\n", p, bytes);
         (pinned[0] ? pinned[1] : pinned[0]) = p;
     }
     bool any() const { return pinned[0] || pinned[1]; }

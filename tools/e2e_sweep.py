@@ -25,7 +25,10 @@ def main() -> None:
     B = 4 * n
     st = hip.stream_create()
     out = {"slots": ish.get_param("staging_slots"), "staging_MiB": ish.get_param("staging_bytes") >> 20}
-    for kind in ("pinned", "pageable"):
+    L = hip.lib()
+    L.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    L.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    for kind in ("pinned", "pageable", "pageable_app_registered"):
         if kind == "pinned":
             hs, hd = hip.host_malloc(B), hip.host_malloc(B)
             xs = np.ctypeslib.as_array((ctypes.c_float * n).from_address(hs))
@@ -33,6 +36,8 @@ def main() -> None:
         else:
             xs, xd = np.zeros(n, np.float32), np.zeros(n, np.float32)
             hs, hd = xs.ctypes.data, xd.ctypes.data
+        if kind == "pageable_app_registered":
+            out["app_register_rc"] = [L.hipHostRegister(hs, B, 0), L.hipHostRegister(hd, B, 0)]
         xs[:] = np.arange(n, dtype=np.float32)
         ts = []
         for rep in range(4):
@@ -50,6 +55,9 @@ def main() -> None:
             del xs, xd
             hip.host_free(hs)
             hip.host_free(hd)
+        if kind == "pageable_app_registered":
+            L.hipHostUnregister(hs)
+            L.hipHostUnregister(hd)
     print(json.dumps(out), flush=True)
     ish.ishmem_finalize()
 
