@@ -543,7 +543,7 @@ bool pageable_host(const void *p)
         (void) hipGetLastError();
         return true;
     }
-    return attr.type == hipMemoryTypeHost && attr.devicePointer == nullptr;
+    return attr.type == hipMemoryTypeUnregistered || (attr.type == hipMemoryTypeHost && attr.devicePointer == nullptr);
 }
 
 struct CallPins {
