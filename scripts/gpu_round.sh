@@ -32,6 +32,8 @@ for s in $STEPS; do
     gpu)    run pytest_gpu 1500 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider ;;
     sel)    run pytest_sel ${SEL_SECS:-1500} python -u -m pytest tests -m gpu -x -v --timeout ${SEL_TIMEOUT:-900} \
                 --timeout-method thread -p no:cacheprovider -k "$SEL" ;;
+    soak)   STRESS_ITERS=${ITERS:-300} STRESS_SEED=${SEED:-9001} STRESS_TIMEOUT=${STRESS_TIMEOUT:-780} run soak ${SOAK_SECS:-900} python -u -m pytest tests/test_gpu_multi.py \
+                -m gpu -x -v --timeout 800 --timeout-method thread -p no:cacheprovider -k randomised_protocol_stress -s ;;
     single) run pytest_single 900 python -m pytest tests/test_gpu_single.py -m gpu -x -q -p no:cacheprovider ;;
     multi)  run pytest_multi 1200 python -m pytest tests/test_gpu_multi.py -m gpu -x -q -p no:cacheprovider ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;

@@ -4,6 +4,7 @@ the driver's).  Every PE checks its dest against the oracle bit-for-bit (canonic
 fold) and against MPICH's MPI_Allreduce golden output (ints / min / max bit-exact; FP sum/prod
 within (p-1)*u*sum|x_i| resp. (p-1)*u*|ref|)."""
 import multiprocessing as mp
+import os
 import queue
 import sys
 import time
@@ -175,7 +176,8 @@ def test_randomised_protocol_stress(npes):
     # shifted), per-PE grid caps and an occupying kernel on a random PE, chained on one stream;
     # every window vs the oracle's fold, guard bytes around it untouched, *ret clean.
     # STRESS_ITERS / STRESS_SEED override (longer soak runs).
-    run_pes(npes, ["stress"], env={"ISHMEM_SYMMETRIC_SIZE": "1G"}, timeout=400)
+    run_pes(npes, ["stress"], env={"ISHMEM_SYMMETRIC_SIZE": "1G"},
+            timeout=float(os.environ.get("STRESS_TIMEOUT", 400)))
 
 
 @pytest.mark.parametrize("npes", [2, 3, 6])
