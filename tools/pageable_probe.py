@@ -27,12 +27,26 @@ def main() -> None:
     d1, d2 = hip.malloc(B), hip.malloc(B)
     s1, s2 = hip.stream_create(), hip.stream_create()
     out = {}
-    for kind in ("pageable", "pinned"):
-        if kind == "pageable":
+    L.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    L.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    L.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    flags = {"pinned": 0, "pinned_noncoherent": 0x80000000, "pinned_coherent": 0x40000000,
+             "pinned_numa_user": 0x20000000}
+    for kind in ("pageable", "registered", *flags):
+        keep = []
+        if kind in ("pageable", "registered"):
             a, b = np.ones(B // 4, np.float32), np.zeros(B // 4, np.float32)
             ha, hb = a.ctypes.data, b.ctypes.data
+            keep = [a, b]
+            if kind == "registered":
+                L.hipHostRegister(ha, B, 0)
+                L.hipHostRegister(hb, B, 0)
         else:
-            ha, hb = hip.host_malloc(B), hip.host_malloc(B)
+            pa, pb = ctypes.c_void_p(), ctypes.c_void_p()
+            if L.hipHostMalloc(ctypes.byref(pa), B, flags[kind]) or L.hipHostMalloc(ctypes.byref(pb), B, flags[kind]):
+                out[kind] = "hipHostMalloc failed"
+                continue
+            ha, hb = pa.value, pb.value
             ctypes.memset(ha, 1, B)
             ctypes.memset(hb, 0, B)
 
@@ -62,16 +76,19 @@ def main() -> None:
         r = {"h2d_GBps": B / timed(h2d) / 1e9, "d2h_GBps": B / timed(d2h) / 1e9,
              "both_threads_GBps_each": B / timed(both) / 1e9}
         r["seq_GBps_each"] = B / timed(lambda: (h2d(), d2h())) / 1e9
+        r["h2d_1GiB_GBps"] = B / timed(lambda: h2d(B)) / 1e9
+        r["d2h_1GiB_GBps"] = B / timed(lambda: d2h(B)) / 1e9
         out[kind] = {k: round(v, 2) for k, v in r.items()}
-        if kind == "pinned":
+        if kind in flags:
             hip.host_free(ha)
             hip.host_free(hb)
+        elif kind == "registered":
+            L.hipHostUnregister(ha)
+            L.hipHostUnregister(hb)
+        del keep
     # hipHostRegister / Unregister of a 1 GiB pageable buffer
     c = np.ones(B // 4, np.float32)
-    reg = getattr(L, "hipHostRegister")
-    unreg = getattr(L, "hipHostUnregister")
-    reg.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
-    unreg.argtypes = [ctypes.c_void_p]
+    reg, unreg = L.hipHostRegister, L.hipHostUnregister
     t0 = time.perf_counter()
     e = reg(c.ctypes.data, B, 0)
     t1 = time.perf_counter()
