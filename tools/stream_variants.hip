@@ -218,6 +218,63 @@ __global__ __launch_bounds__(BS) void split_halves(const f4 *__restrict__ a, con
     }
 }
 
+// Round 3: the multi-PE kernel's reduce-scatter shape — persistent grid, each workgroup a
+// contiguous range, U 16-B items per thread per step from NSRC sources (nt buffer loads), the fold
+// stored write-through (sc0 sc1).  gfx9 waves count loads and stores in ONE in-order vmcnt, so a
+// step that waits for its loads also waits for the previous step's stores to be acknowledged.
+// PIPE: the next step's loads are issued before this step's stores (ping-pong register sets), so
+// the store acknowledgements overlap the next loads.
+template <int NSRC, int U, int BS, bool PIPE>
+__global__ __launch_bounds__(BS) void persist_wt(const f4 *__restrict__ a, const f4 *__restrict__ b,
+                                                 f4 *__restrict__ d, long n)
+{
+    const long TI = (long) BS * U;
+    const long per = ((n + gridDim.x - 1) / gridDim.x + TI - 1) / TI * TI;
+    const long start = (long) blockIdx.x * per, end = min(start + per, n);
+    auto rs = [](const void *p) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short) 0, 0x7FFFFFFF, 0x00020000);
+    };
+    auto load = [&](long t, f4 (&x)[U][2]) {
+        const __amdgpu_buffer_rsrc_t ra = rs(a + t), rb = rs(b + t);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t off = (uint32_t) (u * BS + threadIdx.x) * 16;
+            if (t + u * BS + threadIdx.x < end) {
+                x[u][0] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 2));
+                if (NSRC == 2) x[u][1] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 2));
+            }
+        }
+    };
+    auto store = [&](long t, const f4 (&x)[U][2]) {
+        const __amdgpu_buffer_rsrc_t rd = rs(d + t);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t off = (uint32_t) (u * BS + threadIdx.x) * 16;
+            const f4 v = NSRC == 2 ? x[u][0] + x[u][1] : x[u][0];
+            if (t + u * BS + threadIdx.x < end) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rd, off, 0, 17);
+        }
+    };
+    f4 xa[U][2], xb[U][2];
+    if (!PIPE) {
+        for (long t = start; t < end; t += TI) {
+            load(t, xa);
+            store(t, xa);
+        }
+        return;
+    }
+    long t = start;
+    if (t < end) load(t, xa);
+    while (t < end) {
+        if (t + TI < end) load(t + TI, xb);
+        store(t, xa);
+        t += TI;
+        if (t >= end) break;
+        if (t + TI < end) load(t + TI, xa);
+        store(t, xb);
+        t += TI;
+    }
+}
+
 struct Variant {
     std::string name;
     void (*launch)(const f4 *, const f4 *, f4 *, long, int, hipStream_t);
@@ -289,6 +346,12 @@ void SH(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
 {
     const long g = (n / 2 + BS - 1) / BS;
     hipLaunchKernelGGL((split_halves<BS>), dim3(g), dim3(BS), 0, s, a, b, d, n);
+}
+
+template <int NSRC, int U, int BS, bool PIPE>
+void PW(const f4 *a, const f4 *b, f4 *d, long n, int grid, hipStream_t s)
+{
+    hipLaunchKernelGGL((persist_wt<NSRC, U, BS, PIPE>), dim3(grid), dim3(BS), 0, s, a, b, d, n);
 }
 
 void MC(const f4 *a, const f4 *b, f4 *d, long n, int, hipStream_t s)
@@ -391,6 +454,18 @@ int main(int argc, char **argv)
         vs.push_back({"aux ns2 bs64 ld nt / st sc0sc1 (product a+b)", OA<2, 64, 2, 17>, 0, 2});
         vs.push_back({"  a+b + 8 KiB LDS", OAL<2, 64, 2, 17, 8192>, 0, 2});
         vs.push_back({"  a+b + 16 KiB LDS", OAL<2, 64, 2, 17, 16384>, 0, 2});
+    }
+    if (set == "r3") {  // round 3: store acknowledgements on the persistent kernel's critical path
+        vs.push_back({"aux ns2 bs64 ld nt / st sc0sc1 (product a+b)", OA<2, 64, 2, 17>, 0, 2});
+        vs.push_back({"persist a+b U2 bs256 g1024 plain", PW<2, 2, 256, false>, 1024, 2});
+        vs.push_back({"persist a+b U2 bs256 g1024 PIPE", PW<2, 2, 256, true>, 1024, 2});
+        vs.push_back({"persist a+b U4 bs256 g1024 plain", PW<2, 4, 256, false>, 1024, 2});
+        vs.push_back({"persist a+b U4 bs256 g1024 PIPE", PW<2, 4, 256, true>, 1024, 2});
+        vs.push_back({"persist a+b U2 bs256 g512 PIPE", PW<2, 2, 256, true>, 512, 2});
+        vs.push_back({"persist a+b U2 bs256 g2048 PIPE", PW<2, 2, 256, true>, 2048, 2});
+        vs.push_back({"aux ns1 bs64 ld nt / st sc0sc1 (product copy)", OA<1, 64, 2, 17>, 0, 1});
+        vs.push_back({"persist copy U4 bs256 g1024 plain", PW<1, 4, 256, false>, 1024, 1});
+        vs.push_back({"persist copy U4 bs256 g1024 PIPE", PW<1, 4, 256, true>, 1024, 1});
     }
     hipStream_t s;
     CK(hipStreamCreate(&s));
