@@ -45,15 +45,7 @@ constexpr uint64_t kTile = (uint64_t) kBlock * kUnroll;  // items per tile
 #ifndef ISHMEMI_AR_OCC
 #define ISHMEMI_AR_OCC 4  // multi-PE kernel: workgroups per CU (see allreduce_kernel)
 #endif
-#ifndef ISHMEMI_AR_PIPE
-#define ISHMEMI_AR_PIPE 0  // multi-PE kernel: next step's loads issued before this step's stores
-#endif
-#ifndef ISHMEMI_AR_PIPE_H
-#define ISHMEMI_AR_PIPE_H 1  // pipelined reduce-scatter: items per thread and member per step
-#endif
-#ifndef ISHMEMI_AR_PIPE_AGU
-#define ISHMEMI_AR_PIPE_AGU 2  // pipelined all-gather: items per thread per step
-#endif
+
 
 template <typename T>
 struct alignas(16) Vec {
@@ -516,81 +508,6 @@ __device__ __forceinline__ void rs_tile(const ReduceArgs &a, uint64_t t0, uint64
     }
 }
 
-// A reduce-scatter segment [t0, te) for a compile-time team size P and rotation R, software-
-// pipelined: gfx9 waves count loads AND stores in one in-order vmcnt, so a step that waits for its
-// own loads also waits until the previous step's write-through stores are acknowledged (a
-// round trip to HBM, or over xGMI).  Issuing step k+1's loads before step k's stores (two register
-// sets, ping-pong) takes that acknowledgement off the critical path.
-template <typename T, int OP, bool VEC, int P, int R>
-__device__ __forceinline__ void rs_range_pipe(const ReduceArgs &a, uint64_t t0, uint64_t te,
-                                              uint64_t head_bytes)
-{
-    using Item = std::conditional_t<VEC, Vec<T>, T>;
-    constexpr uint64_t IB = sizeof(Item);
-    constexpr int H = ISHMEMI_AR_PIPE_H;            // items per thread and member per step
-    constexpr uint64_t SI = (uint64_t) H * kBlock;  // items per step
-    const uint32_t tid = threadIdx.x;
-    auto load = [&](uint64_t s0, Item (&x)[H][P]) {
-        const uint32_t lim = (uint32_t) min<uint64_t>(te - s0, SI);
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const int j = (R + k) % P;
-            const char *base = uniform_ptr(a.src[j] + head_bytes + s0 * IB);
-            if (j == a.me) {
-                const Item *lp = (const Item *) base;
-#pragma unroll
-                for (int u = 0; u < H; ++u) {
-                    const uint32_t e = (uint32_t) u * kBlock + tid;
-                    if (e < lim) x[u][k] = lp[e];
-                }
-            } else {
-                const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
-#pragma unroll
-                for (int u = 0; u < H; ++u) {
-                    const uint32_t e = (uint32_t) u * kBlock + tid;
-                    if (e < lim) x[u][k] = cload<Item>(r, e * (uint32_t) IB);
-                }
-            }
-        }
-    };
-    auto fold_store = [&](uint64_t s0, const Item (&x)[H][P]) {
-        const uint32_t lim = (uint32_t) min<uint64_t>(te - s0, SI);
-        const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + head_bytes + s0 * IB));
-#pragma unroll
-        for (int u = 0; u < H; ++u) {
-            Item acc = x[u][(P - R) % P];  // member 0
-#pragma unroll
-            for (int j = 1; j < P; ++j) acc = op1<T, OP>(acc, x[u][(j - R + P) % P]);
-            const uint32_t e = (uint32_t) u * kBlock + tid;
-            if (e < lim) wt_store(dr, e * (uint32_t) IB, acc);
-        }
-    };
-    Item xa[H][P], xb[H][P];
-    uint64_t s0 = t0;
-    if (s0 < te) load(s0, xa);
-    while (s0 < te) {
-        if (s0 + SI < te) load(s0 + SI, xb);
-        fold_store(s0, xa);
-        s0 += SI;
-        if (s0 >= te) break;
-        if (s0 + SI < te) load(s0 + SI, xa);
-        fold_store(s0, xb);
-        s0 += SI;
-    }
-}
-
-template <typename T, int OP, bool VEC, int P, int R = 0>
-__device__ __forceinline__ void rs_range_dispatch(const ReduceArgs &a, int rot, uint64_t t0,
-                                                  uint64_t te, uint64_t head_bytes)
-{
-    if constexpr (R == P - 1) {
-        rs_range_pipe<T, OP, VEC, P, R>(a, t0, te, head_bytes);
-    } else {
-        if (rot == R) rs_range_pipe<T, OP, VEC, P, R>(a, t0, te, head_bytes);
-        else rs_range_dispatch<T, OP, VEC, P, R + 1>(a, rot, t0, te, head_bytes);
-    }
-}
-
 // Wave-uniform run-time rotation -> compile-time rs_tile<R> (a uniform branch per tile).
 template <typename T, int OP, bool VEC, int P, int R = 0>
 __device__ __forceinline__ void rs_tile_dispatch(const ReduceArgs &a, int rot, uint64_t t0,
@@ -761,19 +678,10 @@ __device__ __forceinline__ void rs_segment(const ReduceArgs &a, uint32_t ep, uin
     // tile set, tried, ran 7 % (2 PEs) to 30 % (8 PEs) slower at 1 GiB).
     const int rot = (int) (s % (uint32_t) p);
     const uint64_t ss = cs + (uint64_t) s * a.seg_items, se = min(ss + a.seg_items, ce);
-#if ISHMEMI_AR_PIPE
-    // Two register sets of P members: P = 8 would spill at 4 workgroups per CU (it keeps the
-    // tile loop; its all-gather is pipelined).
-    if constexpr (P > 0 && P <= 4) {
-        if (ss < se) rs_range_dispatch<T, OP, VEC, P>(a, rot, ss, se, head_bytes);
-    } else
-#endif
-    {
-        for (uint64_t t0 = ss; t0 < se; t0 += kTile) {
-            const uint64_t te = min(t0 + kTile, se);
-            if constexpr (P > 0) rs_tile_dispatch<T, OP, VEC, P>(a, rot, t0, te, head_bytes);
-            else rs_tile_any<T, OP, VEC>(a, rot, t0, te, head_bytes);
-        }
+    for (uint64_t t0 = ss; t0 < se; t0 += kTile) {
+        const uint64_t te = min(t0 + kTile, se);
+        if constexpr (P > 0) rs_tile_dispatch<T, OP, VEC, P>(a, rot, t0, te, head_bytes);
+        else rs_tile_any<T, OP, VEC>(a, rot, t0, te, head_bytes);
     }
     (void) nseg;
     // Unaligned head (owned by member 0) and tail (owned by member p-1; one-shot: both by every
@@ -926,11 +834,7 @@ __global__ __launch_bounds__(kBlock, (ar_occ<T, OP, P>())) __attribute__((flatte
                 have_item = false;
                 // The segment's tiles, two per step: 8 loads per lane in flight.
                 const uint64_t ss = js + (uint64_t) s * seg, se = min(ss + seg, je);
-#if ISHMEMI_AR_PIPE
-                constexpr int U = ISHMEMI_AR_PIPE_AGU;
-#else
                 constexpr int U = kAgTiles * kUnroll;
-#endif
                 constexpr uint64_t SI = (uint64_t) U * kBlock;
                 auto ag_load = [&](uint64_t t, Item (&x)[U]) {
                     const uint32_t lim = (uint32_t) min<uint64_t>(se - t, SI);
@@ -950,28 +854,11 @@ __global__ __launch_bounds__(kBlock, (ar_occ<T, OP, P>())) __attribute__((flatte
                         if (k < lim) wt_store(dr, k * (uint32_t) IB, x[u]);
                     }
                 };
-#if ISHMEMI_AR_PIPE
-                // Pipelined like rs_range_pipe: the next step's pulls go out before this step's
-                // stores, so no pull waits for a store acknowledgement.
-                Item xa[U], xb[U];
-                uint64_t t = ss;
-                if (t < se) ag_load(t, xa);
-                while (t < se) {
-                    if (t + SI < se) ag_load(t + SI, xb);
-                    ag_store(t, xa);
-                    t += SI;
-                    if (t >= se) break;
-                    if (t + SI < se) ag_load(t + SI, xa);
-                    ag_store(t, xb);
-                    t += SI;
-                }
-#else
                 for (uint64_t t = ss; t < se; t += SI) {
                     Item x[U];
                     ag_load(t, x);
                     ag_store(t, x);
                 }
-#endif
                 if (VEC && s == 0) {
                     const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
                     const uint64_t rbase = (j == 0 ? 0 : tail_off) * sizeof(T);
