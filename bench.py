@@ -292,6 +292,27 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     return out
 
 
+def link_topology(hip, device: int, world: int) -> list | dict:
+    """Link type and hop count from this GPU to every other rank's GPU (hipExtGetLinkTypeAndHopCount;
+    HSA link types: 2 PCIe, 4 xGMI), so an N > 1 line says what the collective ran over."""
+    names = {0: "hypertransport", 1: "qpi", 2: "pcie", 3: "infiniband", 4: "xgmi"}
+    try:
+        L = hip.lib()
+        fn = L.hipExtGetLinkTypeAndHopCount
+        fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+        out = []
+        for d in range(world):
+            if d == device:
+                continue
+            lt, hc = ctypes.c_uint32(0), ctypes.c_uint32(0)
+            rc = fn(device, d, ctypes.byref(lt), ctypes.byref(hc))
+            out.append({"peer_device": d, "link": names.get(lt.value, str(lt.value)) if rc == 0 else None,
+                        "hops": hc.value if rc == 0 else None, "rc": rc})
+        return out
+    except Exception as ex:
+        return {"error": str(ex)}
+
+
 def xgmi_probe(ish, hip, src, dst, B, world, rank, dist, stream, barrier):
     """Measured link rates (report against the spec AND a measured L).  Plain
     pulls of a peer's source through the local combine kernel, no barriers inside:
@@ -809,6 +830,7 @@ def main() -> int:
                        "parallelism": "1 PE self-reduce" if world == 1 else f"direct RS+AG over {world} PEs"},
             "kernel_ms": kern_ms, "checked": checked, "targets": targets,
             **({"flag_memory": flag_memory} if world > 1 else {}),
+            **({"topology": link_topology(hip, device, world)} if world > 1 and not same_device else {}),
             **({"dev_same_device": True} if same_device else {}), "roofline": roof,
             "cpu_baseline": cpu, **extra,
         }
