@@ -211,6 +211,53 @@ static void pattern_case(size_t n, dim3 block, char *sb, char *db,
     }
 }
 
+// Device-side broadcast (ishmemx_broadcastmem_work_group / ishmem_<TN>_broadcast, the reference's
+// intra-node pull): the source is produced in the kernel, every member pulls the root's bytes.
+__global__ void bcast_kernel(char *dest, char *source, size_t nbytes, int root, int my_pe, int mode, int *rc)
+{
+    for (size_t i = threadIdx.x; i < nbytes; i += blockDim.x) source[i] = (char) (i * 7 + my_pe * 31 + 1);
+    int r;
+    if (mode == 0) {
+        r = ishmemx_broadcastmem_work_group(dest, source, nbytes, root, cg::this_thread_block());
+    } else {
+        __syncthreads();
+        if (threadIdx.x != 0) return;
+        r = ishmem_long_broadcast(ISHMEM_TEAM_WORLD, (long *) dest, (const long *) source, nbytes / 8, root);
+    }
+    if (threadIdx.x == 0) *rc = r;
+}
+
+// Device queries and barriers (src/ishmem.h:54-58, :74-77, :1555-1559).
+__global__ void query_kernel(int *out, char *buf, const char *nonsym)
+{
+    auto grp = cg::this_thread_block();
+    int r = 0;
+    for (int k = 0; k < 5; ++k) ishmemx_team_sync_work_group(ISHMEM_TEAM_WORLD, grp);
+    ishmemx_barrier_all_work_group(grp);
+    ishmemx_sync_all_work_group(grp);
+    if (grp.thread_rank() == 0) {
+        for (int k = 0; k < 5; ++k) r |= ishmem_team_sync(ISHMEM_TEAM_WORLD);
+        ishmem_barrier_all();
+        ishmem_sync_all();
+        const int pe = ishmem_my_pe(), n = ishmem_n_pes();
+        int mj = 0, mn = 0;
+        ishmem_info_get_version(&mj, &mn);
+        char name[ISHMEM_MAX_NAME_LEN];
+        ishmem_info_get_name(name);
+        out[0] = pe;
+        out[1] = n;
+        out[2] = ishmem_team_my_pe(ISHMEM_TEAM_WORLD);
+        out[3] = ishmem_team_n_pes(ISHMEM_TEAM_WORLD);
+        out[4] = ishmem_team_translate_pe(ISHMEM_TEAM_WORLD, (pe + 1) % n, ISHMEM_TEAM_SHARED);
+        out[5] = ishmem_ptr(buf, (pe + 1) % n) != nullptr && ishmem_ptr(buf, n) == nullptr &&
+                 ishmem_ptr(nonsym, 0) == nullptr;
+        out[6] = mj * 10 + mn;
+        out[7] = name[0] != 0;
+        out[8] = r;
+        out[9] = ishmem_team_my_pe(ISHMEMI_C_MAX_TEAMS - 1);  // an unused team slot: -1
+    }
+}
+
 int main()
 {
     ishmem_init();
@@ -300,6 +347,42 @@ int main()
         coll_case<3>(n, 1024, sb, db, rc);
         coll_case<4>(n, 128, sb, db, rc);
         coll_case<5>(n, 64, sb, db, rc);
+    }
+    // Broadcast from every root, work-group and one-work-item forms, odd and even byte counts.
+    for (int root = 0; root < npes; ++root) {
+        for (size_t nb : {(size_t) 8, (size_t) 1000, (size_t) 77777 * 8}) {
+            for (int mode = 0; mode < 2; ++mode) {
+                (void) hipMemset(db, 0, nb + 64);
+                (void) hipMemset(rc, 0xff, sizeof(int));
+                hipLaunchKernelGGL(bcast_kernel, dim3(1), dim3(256), 0, 0, db, sb, nb, root, pe, mode, rc);
+                (void) hipDeviceSynchronize();
+                std::vector<char> got(nb);
+                int r = -1;
+                (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);
+                (void) hipMemcpy(got.data(), db, nb, hipMemcpyDeviceToHost);
+                size_t bad = 0;
+                for (size_t i = 0; i < nb; ++i) bad += got[i] != (char) (i * 7 + root * 31 + 1);
+                if (r != 0 || bad) {
+                    if (++errors <= 16)
+                        printf("[%d] FAIL device broadcast root %d nbytes %zu mode %d rc %d bad %zu\n", pe, root, nb,
+                               mode, r, bad);
+                }
+            }
+        }
+    }
+    {  // queries and barriers
+        int *out = (int *) ishmem_malloc(16 * sizeof(int));
+        char *nonsym = nullptr;
+        (void) hipMalloc(&nonsym, 64);
+        hipLaunchKernelGGL(query_kernel, dim3(1), dim3(256), 0, 0, out, db, nonsym);
+        (void) hipDeviceSynchronize();
+        int q[10];
+        (void) hipMemcpy(q, out, sizeof(q), hipMemcpyDeviceToHost);
+        const int want[10] = {pe, npes, pe, npes, (pe + 1) % npes, 1, 15, 1, 0, -1};
+        for (int k = 0; k < 10; ++k)
+            if (q[k] != want[k] && ++errors <= 16) printf("[%d] FAIL device query %d: %d != %d\n", pe, k, q[k], want[k]);
+        ishmem_free(out);
+        (void) hipFree(nonsym);
     }
     ishmem_free(rc);
     ishmem_free(db);
