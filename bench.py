@@ -115,7 +115,15 @@ def pmc_traffic(kernel_tag: str, nbytes: int):
     return None
 
 
-def roofline(world: int, share: int, B: int, kern_ms: float) -> tuple[dict, float]:
+def multi_pe_kernel(B: int, phased_min: int) -> str:
+    """The multi-PE kernels a B-byte f32 sum takes (runtime.cpp reduce_heap): the phased path's
+    one-shot grids for payloads of at least phased_min bytes (-1: off), else the persistent kernel."""
+    if phased_min >= 0 and B >= phased_min:
+        return "rs_phase_kernel<float,SUM,P> + ag_phase_kernel between 3 one-workgroup team barriers"
+    return "allreduce_kernel<float,SUM,vec>"
+
+
+def roofline(world: int, share: int, B: int, kern_ms: float, kernel: str = "allreduce_kernel<float,SUM,vec>") -> tuple[dict, float]:
     """Roofline of the dominant kernel for one launch of B payload bytes per PE, and the step's
     roofline time t_roof (for the algbw targets).
       world == 1  copy kernel (1-PE reduce = dest = source): 2B of HBM traffic, HBM-bound.
@@ -136,10 +144,11 @@ def roofline(world: int, share: int, B: int, kern_ms: float) -> tuple[dict, floa
         dev_bytes = share * (3.0 - 1.0 / world) * B
         roof = {"bound": "hbm", "achieved": dev_bytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "pes_per_device": share,
-                "traffic": pmc_traffic(f"allreduce_{world}pe_same_device", B) if share == world else None,
+                "traffic": pmc_traffic(f"{'phased' if kernel.startswith('rs_phase') else 'allreduce'}_{world}pe_same_device", B)
+                if share == world else None,
                 "traffic_note": "device-wide FETCH_SIZE (x2) + WRITE_SIZE per launch, all PEs on one GPU "
                                 "(profiles/pmc_summary.json)",
-                "kernel": f"allreduce_kernel<float,SUM,vec> x {share} co-located PEs "
+                "kernel": f"{kernel} x {share} co-located PEs "
                           f"(device HBM traffic {share} x (3 - 1/p) x B per launch)"}
         t_roof = dev_bytes / (HBM_PEAK_GBS * 1e9)
     else:
@@ -148,7 +157,7 @@ def roofline(world: int, share: int, B: int, kern_ms: float) -> tuple[dict, floa
                 "peak": XGMI_LINK_GBS * (world - 1), "unit": "GB/s", "traffic": None,
                 "traffic_note": "no PMC pass of a one-PE-per-GPU run is committed (the round's GPU "
                                 "pool has one GPU per box): HBM traffic per launch unmeasured",
-                "kernel": "allreduce_kernel<float,SUM,vec> (per-PE xGMI ingress 2(p-1)/p*B)"}
+                "kernel": f"{kernel} (per-PE xGMI ingress 2(p-1)/p*B)"}
         t_roof = max((3.0 - 1.0 / world) * B / (HBM_PEAK_GBS * 1e9),
                      (2.0 * B / world) / (XGMI_LINK_GBS * 1e9))
     frac = roof["achieved"] / roof["peak"]
@@ -246,6 +255,8 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     MI355X per PE cannot be rehearsed on a one-GPU box):
       grid  - the payload with the workgroup cap at 128 / 256 / 512 / 1024 (then clamped to the
               resident capacity);
+      phased - the payload on the phased path (one-shot grids between barriers) and on the
+               persistent kernel;
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
       ll    - 4 / 16 / 64 KiB with the one-hop granule path on (default) and off."""
 
@@ -283,6 +294,8 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     for mb in (128, 256, 512, 1024):
         if mb <= cap:
             run("grid", "max_blocks", mb, B, 5)
+    run("phased", "phased_min_bytes", 0, B, 5)
+    run("persistent", "phased_min_bytes", -1, B, 5)
     if world == 2:
         run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
         run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)
@@ -709,7 +722,8 @@ def main() -> int:
     algbw = B / GiB / (ms_per_step / 1000.0)
 
     share = int(ish.get_param("device_share")) if world > 1 else 1
-    roof, t_roof = roofline(world, share, B, kern_ms)
+    roof, t_roof = roofline(world, share, B, kern_ms,
+                            multi_pe_kernel(B, ish.get_param("phased_min_bytes")) if world > 1 else "")
     algbw_roof = B / GiB / t_roof
     targets = {"algbw_roofline_GiBps": algbw_roof, "algbw_frac_of_roofline": algbw / algbw_roof}
     if algbw > algbw_roof:

@@ -152,6 +152,21 @@ struct FaninArgs {
     int nsrc;
 };
 
+// Phased reduce-scatter / all-gather of large payloads (p > 1, 16-B vector body): two one-shot
+// grids that never wait, between one-workgroup team barriers (team_sync_kernel).  Pointers are
+// translated into this process's address space, as in ReduceArgs.
+struct PhaseArgs {
+    const char *src[kMaxPes];   // member j's source (element 0)
+    const char *dstp[kMaxPes];  // member j's dest (element 0)
+    char *dst;                  // own dest
+    uint64_t head, nitems, tail;  // scalar head elements, 16-B body items, scalar tail elements
+    uint64_t items_per_chunk;     // the reduce-scatter partition (a multiple of 64 items)
+    uint32_t elem;                // element bytes (the all-gather copies head / tail bytes)
+    int p, me;
+};
+hipError_t launch_rs_phase(int op, int dt, const PhaseArgs &a, hipStream_t s);
+hipError_t launch_ag_phase(const PhaseArgs &a, hipStream_t s);
+
 // Returns hipSuccess or a launch error.  `vec` selects the 16-B vector body (all operands
 // share the same address residue mod 16) or the element-granular path.
 hipError_t launch_allreduce(int op, int dt, bool vec, const ReduceArgs &a, int grid,

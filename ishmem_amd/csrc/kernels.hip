@@ -14,7 +14,8 @@ int device_share() { return g_device_share; }
     hipError_t launch_allreduce_op##N(int dt, bool vec, const ReduceArgs &a, int grid,             \
                                       hipStream_t s);                                              \
     hipError_t launch_fanin_op##N(int dt, bool vec, const FaninArgs &a, int grid, hipStream_t s); \
-    hipError_t launch_ll_op##N(int dt, const LLArgs &a, hipStream_t s);
+    hipError_t launch_ll_op##N(int dt, const LLArgs &a, hipStream_t s);                            \
+    hipError_t launch_rs_phase_op##N(int dt, const PhaseArgs &a, hipStream_t s);
 ISHMEMI_DECL_OP(0)
 ISHMEMI_DECL_OP(1)
 ISHMEMI_DECL_OP(2)
@@ -66,6 +67,30 @@ hipError_t launch_ll(int op, int dt, const LLArgs &a, hipStream_t s)
         case 6: return launch_ll_op6(dt, a, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_rs_phase(int op, int dt, const PhaseArgs &a, hipStream_t s)
+{
+    if (!op_dtype_valid(op, dt)) return hipErrorInvalidValue;
+    switch (op) {
+        case 0: return launch_rs_phase_op0(dt, a, s);
+        case 1: return launch_rs_phase_op1(dt, a, s);
+        case 2: return launch_rs_phase_op2(dt, a, s);
+        case 3: return launch_rs_phase_op3(dt, a, s);
+        case 4: return launch_rs_phase_op4(dt, a, s);
+        case 5: return launch_rs_phase_op5(dt, a, s);
+        case 6: return launch_rs_phase_op6(dt, a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_ag_phase(const PhaseArgs &a, hipStream_t s)
+{
+    const uint64_t cs = std::min((uint64_t) a.me * a.items_per_chunk, a.nitems);
+    const uint64_t len = std::min(cs + a.items_per_chunk, a.nitems) - cs;
+    hipLaunchKernelGGL(ag_phase_kernel, dim3(phase_grid(ag_phase_kernel, a.nitems - len)), dim3(kFaninBlock),
+                       0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_team_sync(const ReduceArgs &a, hipStream_t s)

@@ -940,6 +940,165 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
 }
 
 // ---------------------------------------------------------------------------------------------
+// Phased reduce-scatter + all-gather for large payloads (runtime.cpp reduce_heap, p > 1, 16-B
+// vector body, payload >= ISHMEM_PHASED_MIN_BYTES):
+//   team_sync_kernel - every member's source is final;
+//   rs_phase_kernel  - dst[chunk me] = fold_j src_j[chunk me] in canonical team order: ONE 16-B
+//                      item per thread, one-wave workgroups, a one-shot grid — the fan-in kernel's
+//                      shape (83 % of HBM on the same 2-read-1-write traffic) instead of the
+//                      persistent kernel's segment loop (4.7 TB/s in its reduce-scatter phase,
+//                      DESIGN.md §3); peers' items by system-coherent loads, the load order rotated
+//                      per workgroup so concurrently running workgroups pull from every member;
+//   team_sync_kernel - every member's chunk is stored (kernel boundary: the write-through stores
+//                      have completed) and every member has finished reading the sources;
+//   ag_phase_kernel  - dst[chunk j] = dst_j[chunk j] for every j != me;
+//   team_sync_kernel - every member has finished reading this member's dest.
+// Neither grid ever waits, so any residency works and co-located PEs cannot crowd each other
+// out; the only waiters are the three one-workgroup barriers.  In place is safe: member j reads
+// chunk j of my source only in its reduce-scatter, and my all-gather (the only writer of chunk j
+// here) starts after the middle barrier.  The price is two more launches and two more barrier
+// round trips than the persistent kernel (~10 us), so it is used for large payloads only.
+// ---------------------------------------------------------------------------------------------
+template <typename T, int OP, int P, int R>
+__device__ __forceinline__ void rs_phase_item(const PhaseArgs &a, uint64_t wb, bool valid)
+{
+    using Item = Vec<T>;
+    const uint32_t off = threadIdx.x * 16u;
+    Item x[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int j = (R + k) % P;
+        if (!valid) continue;
+        if (j == a.me) x[k] = nt_load((const Item *) (a.src[j] + wb + off));
+        else x[k] = cload<Item>(make_rsrc(uniform_ptr(a.src[j] + wb)), off);
+    }
+    Item acc = x[(P - R) % P];  // member 0
+#pragma unroll
+    for (int j = 1; j < P; ++j) acc = op1<T, OP>(acc, x[(j - R + P) % P]);
+    if (valid) wt_store(make_rsrc(uniform_ptr(a.dst + wb)), off, acc);
+}
+
+template <typename T, int OP, int P, int R = 0>
+__device__ __forceinline__ void rs_phase_dispatch(const PhaseArgs &a, int rot, uint64_t wb, bool valid)
+{
+    if constexpr (R == P - 1) {
+        rs_phase_item<T, OP, P, R>(a, wb, valid);
+    } else {
+        if (rot == R) rs_phase_item<T, OP, P, R>(a, wb, valid);
+        else rs_phase_dispatch<T, OP, P, R + 1>(a, rot, wb, valid);
+    }
+}
+
+// P = 0: any team size, loaded and folded in team order.
+template <typename T, int OP>
+__device__ __forceinline__ void rs_phase_item_any(const PhaseArgs &a, uint64_t wb, bool valid)
+{
+    using Item = Vec<T>;
+    if (!valid) return;
+    const uint32_t off = threadIdx.x * 16u;
+    Item acc;
+    for (int j = 0; j < a.p; ++j) {
+        Item x;
+        if (j == a.me) x = nt_load((const Item *) (a.src[j] + wb + off));
+        else x = cload<Item>(make_rsrc(uniform_ptr(a.src[j] + wb)), off);
+        acc = j == 0 ? x : op1<T, OP>(acc, x);
+    }
+    wt_store(make_rsrc(uniform_ptr(a.dst + wb)), off, acc);
+}
+
+template <typename T, int OP, int P>
+__global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
+{
+    const int p = a.p, me = a.me;
+    const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
+    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
+    const uint64_t head_bytes = a.head * sizeof(T);
+    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
+    for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kFaninBlock; i0 < ce; i0 += stride) {
+        const bool valid = i0 + threadIdx.x < ce;
+        const uint64_t wb = head_bytes + i0 * 16;
+        if constexpr (P > 0) rs_phase_dispatch<T, OP, P>(a, (int) ((i0 / kFaninBlock) % P), wb, valid);
+        else rs_phase_item_any<T, OP>(a, wb, valid);
+    }
+    // Unaligned head (member 0's) and tail (member p-1's), element-wise, by workgroup 0;
+    // descriptors based at the region (offsets < 16 B).
+    if (blockIdx.x == 0) {
+        const int tid = threadIdx.x;
+        const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
+        for (int region = 0; region < 2; ++region) {
+            const bool owner = region == 0 ? me == 0 : me == p - 1;
+            const uint64_t cnt = region == 0 ? a.head : a.tail;
+            if (!owner || (uint64_t) tid >= cnt) continue;
+            const uint64_t rbase = (region == 0 ? 0 : tail_off) * sizeof(T);
+            const uint32_t off = (uint32_t) (tid * sizeof(T));
+            T acc = T();
+            for (int j = 0; j < p; ++j) {
+                T x;
+                if (j == me) x = ((const T *) (a.src[j] + rbase))[tid];
+                else x = cload<T>(make_rsrc(uniform_ptr(a.src[j] + rbase)), off);
+                acc = (j == 0) ? x : op1<T, OP>(acc, x);
+            }
+            wt_store(make_rsrc(uniform_ptr(a.dst + rbase)), off, acc);
+        }
+    }
+}
+
+// Every item outside chunk `me`, pulled from its owner's dest.  Item g of the grid's range maps
+// to array item i = g (before chunk me) or g + |chunk me| (after it); chunk edges are multiples
+// of 64 items, so a workgroup's 64 items never straddle two owners.
+__global__ __launch_bounds__(kFaninBlock) void ag_phase_kernel(PhaseArgs a)
+{
+    const int p = a.p, me = a.me;
+    const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
+    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
+    const uint64_t total = a.nitems - (ce - cs);
+    const uint64_t head_bytes = a.head * a.elem;
+    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
+    const uint32_t off = threadIdx.x * 16u;
+    for (uint64_t g0 = (uint64_t) blockIdx.x * kFaninBlock; g0 < total; g0 += stride) {
+        const uint64_t i0 = g0 < cs ? g0 : g0 + (ce - cs);
+        const int j = (int) __builtin_amdgcn_readfirstlane((uint32_t) (i0 / a.items_per_chunk));
+        if (g0 + threadIdx.x < total) {
+            const uint64_t wb = head_bytes + i0 * 16;
+            const u32x4 x = cload<u32x4>(make_rsrc(uniform_ptr(a.dstp[j] + wb)), off);
+            wt_store(make_rsrc(uniform_ptr(a.dst + wb)), off, x);
+        }
+    }
+    if (blockIdx.x == 0) {
+        // Head bytes from member 0, tail bytes from member p-1 (byte copies, < 16 each).
+        const uint32_t tid = threadIdx.x;
+        const uint64_t tail_b = (uint64_t) a.tail * a.elem;
+        const uint64_t tail_base = head_bytes + a.nitems * 16;
+        if (me != 0 && tid < head_bytes)
+            a.dst[tid] = (char) cload<uint8_t>(make_rsrc(uniform_ptr(a.dstp[0])), tid);
+        if (me != p - 1 && tid < tail_b)
+            a.dst[tail_base + tid] = (char) cload<uint8_t>(make_rsrc(uniform_ptr(a.dstp[p - 1] + tail_base)), tid);
+    }
+}
+
+template <typename K>
+int phase_grid(K, uint64_t items)
+{
+    const uint64_t g = (items + kFaninBlock - 1) / kFaninBlock;
+    return (int) std::max<uint64_t>(1, std::min<uint64_t>(g, (uint64_t) kFaninMaxGrid));
+}
+
+template <typename T, int OP>
+hipError_t rs_phase_t(const PhaseArgs &a, hipStream_t s)
+{
+    const uint64_t cs = std::min((uint64_t) a.me * a.items_per_chunk, a.nitems);
+    const uint64_t len = std::min(cs + a.items_per_chunk, a.nitems) - cs;
+    auto go = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(phase_grid(kernel, len)), dim3(kFaninBlock), 0, s, a);
+    };
+    if (a.p == 2) go(rs_phase_kernel<T, OP, 2>);
+    else if (a.p == 4) go(rs_phase_kernel<T, OP, 4>);
+    else if (a.p == 8) go(rs_phase_kernel<T, OP, 8>);
+    else go(rs_phase_kernel<T, OP, 0>);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Small-message path: one data hop, no barriers.  Thread t owns 8 payload bytes (item t): it
 // pushes them as two {data, epoch} granules into slot `me` of every peer's ring (system-scope
 // 8-B atomic stores into fine-grained memory: a granule is its own flag, MI355X_MICROARCH.md

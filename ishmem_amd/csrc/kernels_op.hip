@@ -24,6 +24,12 @@ hipError_t ISHMEMI_CAT(launch_fanin_op, ISHMEMI_KOP)(int dt, bool vec, const Fan
     return dispatch_dt<ISHMEMI_KOP, FaninArgs>(dt, l);
 }
 
+hipError_t ISHMEMI_CAT(launch_rs_phase_op, ISHMEMI_KOP)(int dt, const PhaseArgs &a, hipStream_t s)
+{
+    auto l = [&]<typename T, int OP>() { return rs_phase_t<T, OP>(a, s); };
+    return dispatch_dt<ISHMEMI_KOP, PhaseArgs>(dt, l);
+}
+
 hipError_t ISHMEMI_CAT(launch_ll_op, ISHMEMI_KOP)(int dt, const LLArgs &a, hipStream_t s)
 {
     auto l = [&]<typename T, int OP>() { return ll_t<T, OP>(a, s); };

@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <limits>
 #include <map>
 #include <mutex>
 #include <string>
@@ -91,6 +92,12 @@ struct Team {
     int num_contexts = 0;                 // ishmem_team_config_t given at split (reported only)
 };
 
+constexpr long long kPhasedOff = std::numeric_limits<long long>::max();
+// Measured (profiles/r03/phased/): 2 PEs x 1 GiB 0.84 ms phased against
+// 0.99-1.13 ms persistent, 128 MiB 110 vs 145 us; below 64 MiB the two extra barrier round trips
+// cost more than the one-shot grids save.
+constexpr long long kPhasedDefault = 128ll << 20;
+
 struct PeRecord {
     int32_t pe, pid, device, flags_kind;
     int32_t flags_kind_requested;  // ISHMEM_FLAGS_KIND (tests): where this PE's ladder started
@@ -98,7 +105,7 @@ struct PeRecord {
     uint64_t heap_size;
     // Launch-shape parameters: the multi-PE kernels pair workgroup b with workgroup b of every
     // peer and choose the LL path per call, so every PE must use the same values.
-    int64_t max_blocks, ll_max_bytes, oneshot_p2;
+    int64_t max_blocks, ll_max_bytes, oneshot_p2, phased_min;
     uint64_t staging_bytes;
     int64_t staging_slots;
     hipIpcMemHandle_t heap_handle;
@@ -140,6 +147,10 @@ struct State {
     // (ISHMEM_ONESHOT_P2_MAX_BYTES; above it the barrier saved is noise and RS + AG's lower HBM
     // traffic wins where HBM, not the link, bounds).
     long long oneshot_p2 = 64ll << 20;
+    // Payloads of at least this many bytes (16-B vector body) take the phased reduce-scatter /
+    // all-gather (two one-shot grids between one-workgroup barriers, kernels_impl.h) instead of
+    // the persistent kernel (ISHMEM_PHASED_MIN_BYTES; kPhasedOff disables it).
+    long long phased_min = kPhasedDefault;
     hipEvent_t order_ev = nullptr;
     // Completion of the last use of the staging region (staged pipeline or scan scratch); the
     // next user waits on it, whatever stream it runs on.
@@ -523,6 +534,29 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         a.seg_items = seg_items(pl.nitems);
         pl.grid = (int) std::max<uint64_t>(
             1, std::min<uint64_t>(nsegs(pl.nitems, a.seg_items), (uint64_t) s.max_blocks));
+    } else if (pl.vec && (long long) nb >= s.phased_min) {
+        // Large payloads: barrier, one-shot reduce-scatter, barrier, one-shot all-gather, barrier
+        // (kernels_impl.h, "Phased reduce-scatter + all-gather").  The barriers carry *ret.
+        PhaseArgs ph;
+        memset(&ph, 0, sizeof(ph));
+        for (int j = 0; j < t.size; ++j) {
+            ph.src[j] = a.src[j];
+            ph.dstp[j] = a.dstp[j];
+        }
+        ph.dst = a.dst;
+        ph.head = pl.head;
+        ph.nitems = pl.nitems;
+        ph.tail = pl.tail;
+        ph.items_per_chunk = pl.items_per_chunk;
+        ph.elem = (uint32_t) es;
+        ph.p = t.size;
+        ph.me = t.my_idx;
+        HIP_TRY(launch_team_sync(a, st));
+        HIP_TRY(launch_rs_phase(op, dt, ph, st));
+        HIP_TRY(launch_team_sync(a, st));
+        HIP_TRY(launch_ag_phase(ph, st));
+        HIP_TRY(launch_team_sync(a, st));
+        return 0;
     }
     HIP_TRY(launch_allreduce(op, dt, pl.vec, a, pl.grid, st));
     return 0;
@@ -1072,6 +1106,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.trace = nullptr;
     s.stream_order = env_ll("ISHMEM_STREAM_ORDER", 0) != 0;
     s.oneshot_p2 = std::max<long long>(0, env_ll("ISHMEM_ONESHOT_P2_MAX_BYTES", 64ll << 20));
+    s.phased_min = env_ll("ISHMEM_PHASED_MIN_BYTES", kPhasedDefault);
+    if (s.phased_min < 0) s.phased_min = kPhasedOff;
     s.staging_bytes = (parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20) + kHeapAlign - 1) &
                       ~(size_t) (kHeapAlign - 1);
     s.staging_slots = (int) std::min<long long>(kMaxStagingSlots, std::max<long long>(2, env_ll("ISHMEM_STAGING_SLOTS", 4)));
@@ -1128,6 +1164,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.max_blocks = s.max_blocks;
         mine.ll_max_bytes = s.ll_max_bytes;
         mine.oneshot_p2 = s.oneshot_p2;
+        mine.phased_min = s.phased_min;
         mine.staging_bytes = s.staging_bytes;
         mine.staging_slots = s.staging_slots;
         if (hipDeviceGetPCIBusId(mine.pci_bus, sizeof(mine.pci_bus), s.device) != hipSuccess) {
@@ -1148,6 +1185,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         for (int j = 0; j < npes; ++j) {
             s.ll_max_bytes = std::min<long long>(s.ll_max_bytes, all[j].ll_max_bytes);
             s.oneshot_p2 = std::min<long long>(s.oneshot_p2, all[j].oneshot_p2);
+            s.phased_min = std::max<long long>(s.phased_min, all[j].phased_min);
             s.staging_bytes = std::min<size_t>(s.staging_bytes, all[j].staging_bytes);
             s.staging_slots = (int) std::min<int64_t>(s.staging_slots, all[j].staging_slots);
         }
@@ -2022,6 +2060,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
     else if (n == "stream_order") s.stream_order = value != 0;
     else if (n == "oneshot_p2_max_bytes") s.oneshot_p2 = std::max<long long>(0, value);
+    else if (n == "phased_min_bytes") s.phased_min = value < 0 ? kPhasedOff : value;
     else if (n == "ll_max_bytes") s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes, std::max<long long>(0, value));
     else if (n == "debug") s.debug = (int) value;
     else if (n == "trace_buffer") s.trace = (uint64_t *) (uintptr_t) value;
@@ -2037,6 +2076,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "timeout_ms") return s.timeout_ms;
     if (n == "stream_order") return s.stream_order ? 1 : 0;
     if (n == "oneshot_p2_max_bytes") return s.oneshot_p2;
+    if (n == "phased_min_bytes") return s.phased_min == kPhasedOff ? -1 : s.phased_min;
     if (n == "ll_max_bytes") return s.ll_max_bytes;
     if (n == "debug") return s.debug;
     if (n == "flags_fine_grained") return s.flags_kind != kFlagsCoarse ? 1 : 0;

@@ -60,3 +60,17 @@ def test_roofline_one_pe_per_gpu_is_xgmi_and_flags_a_violated_model():
     one, t1 = b.roofline(1, 1, B, 0.3174)
     assert one["bound"] == "hbm" and abs(one["frac"] - 2 * B / 0.3174e-3 / 1e9 / 8000) < 1e-9
     assert abs(t1 - 2 * B / 8e12) < 1e-12
+
+
+def test_multi_pe_kernel_follows_the_phased_threshold():
+    # runtime.cpp reduce_heap: payloads of at least phased_min_bytes take the phased path's two
+    # one-shot grids (-1: off); the roofline names them, and a same-device line then looks up the
+    # phased path's PMC entry (the persistent kernel's would not describe the kernels that ran).
+    b = _bench()
+    B = 1 << 30
+    k = b.multi_pe_kernel(B, 128 << 20)
+    assert k.startswith("rs_phase_kernel")
+    assert b.multi_pe_kernel(B, -1).startswith("allreduce_kernel")
+    assert b.multi_pe_kernel(64 << 20, 128 << 20).startswith("allreduce_kernel")
+    roof, _ = b.roofline(2, 2, B, 0.84, k)
+    assert roof["kernel"].startswith("rs_phase_kernel") and 0 < roof["frac"] <= 1

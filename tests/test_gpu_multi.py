@@ -126,6 +126,19 @@ def test_two_pe_reduce_scatter_allgather_path():
             env={"ISHMEM_ONESHOT_P2_MAX_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_MAX_BLOCKS": 64})
 
 
+@pytest.mark.parametrize("npes", [2, 3, 4, 8])
+def test_phased_reduce_scatter_allgather_path(npes):
+    # The phased path (barrier, one-shot reduce-scatter grid, barrier, one-shot all-gather grid,
+    # barrier) forced for every heap reduce with a 16-B body — no LL, no two-member one-shot fold:
+    # the golden inputs (every op / type), in place, the offset sweep (head / tail elements, empty
+    # chunks), edge cases, 256 MiB per PE compared in full, hipGraph replay and the chained-
+    # producer coherence tripwire.  p = 3 runs the run-time team-size fold.
+    run_pes(npes, ["golden", "inplace", "offsets", "edge", "large", "graph", "tripwire"],
+            env={"ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_ONESHOT_P2_MAX_BYTES": 0,
+                 "ISHMEM_MAX_BLOCKS": 64},
+            timeout=400)
+
+
 def test_reduce_completes_while_another_kernel_holds_most_cus():
     # Weakness of the round-1 protocol (workgroup b of every PE paired with workgroup b of every
     # peer): a collective whose partner workgroups cannot all be resident.  Now any workgroup may
