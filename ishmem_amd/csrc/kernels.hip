@@ -86,10 +86,10 @@ hipError_t launch_rs_phase(int op, int dt, const PhaseArgs &a, hipStream_t s)
 
 hipError_t launch_ag_phase(const PhaseArgs &a, hipStream_t s)
 {
-    const uint64_t cs = std::min((uint64_t) a.me * a.items_per_chunk, a.nitems);
-    const uint64_t len = std::min(cs + a.items_per_chunk, a.nitems) - cs;
-    hipLaunchKernelGGL(ag_phase_kernel, dim3(phase_grid(ag_phase_kernel, a.nitems - len)), dim3(kFaninBlock),
-                       0, s, a);
+    // One workgroup per (peer, 64-item block) of a full chunk (ag_phase_kernel's work list).
+    const uint64_t blocks = (a.items_per_chunk + kFaninBlock - 1) / kFaninBlock;
+    hipLaunchKernelGGL(ag_phase_kernel, dim3(phase_grid(ag_phase_kernel, (uint64_t) (a.p - 1) * blocks * kFaninBlock)),
+                       dim3(kFaninBlock), 0, s, a);
     return hipGetLastError();
 }
 

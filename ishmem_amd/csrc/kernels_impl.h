@@ -1043,22 +1043,25 @@ __global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
     }
 }
 
-// Every item outside chunk `me`, pulled from its owner's dest.  Item g of the grid's range maps
-// to array item i = g (before chunk me) or g + |chunk me| (after it); chunk edges are multiples
-// of 64 items, so a workgroup's 64 items never straddle two owners.
+// Every item outside chunk `me`, pulled from its owner's dest.  Workgroup w takes peer
+// k = w mod (p-1) (member (me + 1 + k) mod p) and that member's 64-item block w / (p-1):
+// consecutive workgroups — the ones resident together in a one-shot grid — pull from every peer
+// at once, so every xGMI link is busy (in chunk order the resident window, a few MiB, would sit
+// inside one peer's chunk and load one link at a time).  Chunk edges are multiples of 64 items.
 __global__ __launch_bounds__(kFaninBlock) void ag_phase_kernel(PhaseArgs a)
 {
     const int p = a.p, me = a.me;
-    const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
-    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
-    const uint64_t total = a.nitems - (ce - cs);
     const uint64_t head_bytes = a.head * a.elem;
-    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
+    const uint64_t peers = (uint64_t) (p - 1);
+    const uint64_t blocks = (a.items_per_chunk + kFaninBlock - 1) / kFaninBlock;  // per chunk
+    const uint64_t work = peers * blocks;
     const uint32_t off = threadIdx.x * 16u;
-    for (uint64_t g0 = (uint64_t) blockIdx.x * kFaninBlock; g0 < total; g0 += stride) {
-        const uint64_t i0 = g0 < cs ? g0 : g0 + (ce - cs);
-        const int j = (int) __builtin_amdgcn_readfirstlane((uint32_t) (i0 / a.items_per_chunk));
-        if (g0 + threadIdx.x < total) {
+    for (uint64_t w = blockIdx.x; w < work; w += gridDim.x) {
+        const int j = (me + 1 + (int) (w % peers)) % p;
+        const uint64_t js = min((uint64_t) j * a.items_per_chunk, a.nitems);
+        const uint64_t je = min(js + a.items_per_chunk, a.nitems);
+        const uint64_t i0 = js + (w / peers) * kFaninBlock;
+        if (i0 + threadIdx.x < je) {
             const uint64_t wb = head_bytes + i0 * 16;
             const u32x4 x = cload<u32x4>(make_rsrc(uniform_ptr(a.dstp[j] + wb)), off);
             wt_store(make_rsrc(uniform_ptr(a.dst + wb)), off, x);
