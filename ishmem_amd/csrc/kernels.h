@@ -125,6 +125,8 @@ struct CollectArgs {
 };
 hipError_t launch_collect(const CollectArgs &a, int grid, hipStream_t s);
 hipError_t launch_collect_dyn(const CollectArgs &a, int grid, hipStream_t s);
+// Phased collect: one-shot pull grid, to be bracketed by launch_team_sync on the same stream.
+hipError_t launch_collect_phase(const CollectArgs &a, hipStream_t s);
 
 // Inclusive / exclusive prefix sum across the team (MPI_Scan / MPI_Exscan semantics).
 struct ScanArgs {

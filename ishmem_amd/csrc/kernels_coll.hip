@@ -57,6 +57,51 @@ __global__ __launch_bounds__(kBlock) void collect_kernel(CollectArgs a)
     launch_finish(a, ep);
 }
 
+// Phased fcollect / collect (runtime.cpp collect_launch, total bytes >= ISHMEM_PHASED_MIN_BYTES):
+// team_sync_kernel, this one-shot grid, team_sync_kernel — the reduce's phased shape
+// (kernels_impl.h).  One 1 KiB block of one member per one-wave workgroup, 16 / U items per
+// thread (item k * 64 + lane: every load instruction is one contiguous 64 * U bytes); workgroup w
+// takes member (me + 1 + w mod p) mod p and that member's block w / p, so the resident window
+// pulls from every member (every link) at once.  Never waits: any residency works.
+template <int U>
+__global__ __launch_bounds__(kFaninBlock) void collect_phase_kernel(CollectArgs a, uint64_t blocks)
+{
+    using Item = std::conditional_t<U == 16, Vec<uint32_t>, std::conditional_t<U == 4, uint32_t, uint8_t>>;
+    constexpr int K = 16 / U;
+    constexpr uint64_t kBlockItems = (uint64_t) kFaninBlock * K;  // 1 KiB
+    const int p = a.p;
+    const uint32_t lane = threadIdx.x;
+    for (uint64_t w = blockIdx.x; w < (uint64_t) p * blocks; w += gridDim.x) {
+        const int j = (a.me + 1 + (int) (w % (uint64_t) p)) % p;
+        const uint64_t nitems = a.nbytes[j] / U;
+        const uint64_t i0 = (w / (uint64_t) p) * kBlockItems;
+        if (i0 >= nitems) continue;
+        const uint32_t lim = (uint32_t) min<uint64_t>(nitems - i0, kBlockItems);
+        const char *base = uniform_ptr(a.src[j] + i0 * U);
+        Item x[K];
+        if (j == a.me) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t e = (uint32_t) k * kFaninBlock + lane;
+                if (e < lim) x[k] = nt_load((const Item *) base + e);
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(base);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t e = (uint32_t) k * kFaninBlock + lane;
+                if (e < lim) x[k] = cload<Item>(r, e * (uint32_t) U);
+            }
+        }
+        const __amdgpu_buffer_rsrc_t dr = make_rsrc(uniform_ptr(a.dst + a.dst_off[j] + i0 * U));
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t e = (uint32_t) k * kFaninBlock + lane;
+            if (e < lim) wt_store(dr, e * (uint32_t) U, x[k]);
+        }
+    }
+}
+
 // Member j's `nbytes` at `src` -> dst (local), U-byte items, tiles b, b + G, ... of workgroup b.
 template <int U>
 __device__ __forceinline__ void collect_member(const char *src, char *dst, uint64_t nbytes, bool local,
@@ -329,6 +374,18 @@ hipError_t launch_collect(const CollectArgs &a, int grid, hipStream_t s)
     if (a.unit == 16) return launch_res(collect_kernel<16>, a, grid, s);
     if (a.unit == 4) return launch_res(collect_kernel<4>, a, grid, s);
     return launch_res(collect_kernel<1>, a, grid, s);
+}
+
+hipError_t launch_collect_phase(const CollectArgs &a, hipStream_t s)
+{
+    uint64_t maxb = 0;
+    for (int j = 0; j < a.p; ++j) maxb = std::max<uint64_t>(maxb, a.nbytes[j]);
+    const uint64_t blocks = (maxb + 1023) / 1024;  // 1 KiB blocks of the largest member
+    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t) a.p * blocks, (uint64_t) kFaninMaxGrid));
+    if (a.unit == 16) hipLaunchKernelGGL(collect_phase_kernel<16>, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
+    else if (a.unit == 4) hipLaunchKernelGGL(collect_phase_kernel<4>, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
+    else hipLaunchKernelGGL(collect_phase_kernel<1>, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
+    return hipGetLastError();
 }
 
 hipError_t launch_collect_dyn(const CollectArgs &a, int grid, hipStream_t s)

@@ -732,6 +732,17 @@ int collect_launch(State &s, int team, void *dst, const void *src, const uint64_
     a.dst = (char *) dst;
     a.ret = ret;
     a.unit = (orv & 15) == 0 ? 16 : (orv & 3) == 0 ? 4 : 1;
+    if (t.size > 1 && (long long) off >= s.phased_min) {
+        // Large: barrier, one-shot pull grid, barrier (kernels_coll.hip collect_phase_kernel).
+        // Decided on the total bytes only, which every member knows, so all take the same path.
+        ReduceArgs r;
+        if (team_args(s, team, r, why)) return fail("collect: " + why);
+        r.ret = ret;
+        HIP_TRY(launch_team_sync(r, st));
+        HIP_TRY(launch_collect_phase(a, st));
+        HIP_TRY(launch_team_sync(r, st));
+        return 0;
+    }
     const uint64_t items = maxb / a.unit, tile = (uint64_t) kBlock * kUnroll;
     const int grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((items + tile - 1) / tile, s.max_blocks));
     HIP_TRY(launch_collect(a, grid, st));

@@ -32,6 +32,24 @@ for s in $STEPS; do
       done
     done
     unset ISHMEM_PHASED_MIN_BYTES ISHMEM_BENCH_SAME_DEVICE ;;
+  colltests)
+    ISHMEM_PHASED_MIN_BYTES=0 timeout -k 10 900 python -u -m pytest tests/test_gpu_multi.py tests/test_examples.py tests/test_gpu_cpp.py \
+      -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider \
+      -k "collect or bcast or teams or team or example or patterns or device" \
+      > $OUT/pytest_phased_coll.log 2>&1 || { tail -30 $OUT/pytest_phased_coll.log; exit 1; }
+    tail -3 $OUT/pytest_phased_coll.log ;;
+  collsweep)
+    export ISHMEM_BENCH_SAME_DEVICE=1
+    for np_ in 2 8; do
+      for v in base phased; do
+        if [ $v = phased ]; then export ISHMEM_PHASED_MIN_BYTES=0; else export ISHMEM_PHASED_MIN_BYTES=-1; fi
+        timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np_ --master-addr 127.0.0.1 \
+          --master-port 2962$np_ tools/sweep.py --coll fcollect --max-mib $((512 / np_)) --min-bytes 1048576 --factor 4 --iters 20 \
+          > $OUT/coll_${v}_p$np_.csv 2> $OUT/coll_${v}_p$np_.err || exit $?
+        echo "== fcollect $v p$np_"; grep -v Gloo $OUT/coll_${v}_p$np_.csv
+      done
+    done
+    unset ISHMEM_PHASED_MIN_BYTES ISHMEM_BENCH_SAME_DEVICE ;;
   sweep)
     export ISHMEM_BENCH_SAME_DEVICE=1
     for np_ in 2 8; do
