@@ -305,6 +305,74 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a)
     launch_finish(a, ep);
 }
 
+// Phased scan (runtime.cpp scan_impl, segments of >= ISHMEM_PHASED_MIN_BYTES): per segment
+// team_sync_kernel, scan_p1_kernel, team_sync_kernel, scan_p2_kernel, team_sync_kernel — the
+// reduce's phased shape (kernels_impl.h).  Phase 1: one item of chunk me per thread of a one-shot
+// grid of one-wave workgroups, every member's prefix into this PE's scratch row k; phase 2:
+// workgroup w pulls block w / p of its row of member c = (me + 1 + w mod p) mod p's scratch
+// (every member, every link, at once).  Neither grid waits; the barriers order the phases, and the
+// last one protects the scratch rows from the next segment.
+template <typename T, bool VEC, int P>
+__global__ __launch_bounds__(kFaninBlock) void scan_p1_kernel(ScanArgs a)
+{
+    using I = std::conditional_t<VEC, Vec<T>, T>;
+    constexpr uint64_t E = sizeof(I) / sizeof(T);
+    const int p = P > 0 ? P : a.p, me = a.me;
+    const uint64_t ipc = a.items_per_chunk;
+    const uint64_t cs = min((uint64_t) me * ipc, a.nelems), ce = min(cs + ipc, a.nelems);
+    const uint64_t nI = (ce - cs) / E;
+    const uint64_t tail = (ce - cs) - nI * E;  // < E elements, last chunk only
+    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
+    const uint32_t lane = threadIdx.x;
+    for (uint64_t t0 = (uint64_t) blockIdx.x * kFaninBlock; t0 < nI; t0 += stride) {
+        const char *base[kMaxPes];
+        char *row[kMaxPes];
+        for (int k = 0; k < p; ++k) {
+            base[k] = uniform_ptr(a.src[k] + (cs + t0 * E) * sizeof(T));
+            row[k] = (char *) uniform_ptr(a.scratch[me] + ((uint64_t) k * ipc + t0 * E) * sizeof(T));
+        }
+        scan_item_fold<T, I, P>(a, base, row, lane * (uint32_t) sizeof(I), p, me, t0 + lane < nI);
+    }
+    if (tail && blockIdx.x == 0 && lane < tail) {
+        const char *base[kMaxPes];
+        char *row[kMaxPes];
+        for (int k = 0; k < p; ++k) {
+            base[k] = uniform_ptr(a.src[k] + (cs + nI * E) * sizeof(T));
+            row[k] = (char *) uniform_ptr(a.scratch[me] + ((uint64_t) k * ipc + nI * E) * sizeof(T));
+        }
+        scan_item_fold<T, T, 0>(a, base, row, lane * (uint32_t) sizeof(T), p, me, true);
+    }
+}
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kFaninBlock) void scan_p2_kernel(ScanArgs a, uint64_t blocks)
+{
+    using I = std::conditional_t<VEC, Vec<T>, T>;
+    constexpr uint64_t E = sizeof(I) / sizeof(T);
+    const int p = a.p, me = a.me;
+    const uint64_t ipc = a.items_per_chunk;
+    const uint32_t lane = threadIdx.x;
+    for (uint64_t w = blockIdx.x; w < (uint64_t) p * blocks; w += gridDim.x) {
+        const int c = (me + 1 + (int) (w % (uint64_t) p)) % p;
+        const uint64_t cs = min((uint64_t) c * ipc, a.nelems), ce = min(cs + ipc, a.nelems);
+        const uint64_t nI = (ce - cs) / E;
+        const uint64_t t0 = (w / (uint64_t) p) * kFaninBlock;
+        const char *rowbase = a.scratch[c] + (uint64_t) me * ipc * sizeof(T);
+        if (t0 < nI) {
+            if (t0 + lane < nI) {
+                const I x = cload<I>(make_rsrc(uniform_ptr(rowbase + t0 * E * sizeof(T))), lane * (uint32_t) sizeof(I));
+                wt_store(make_rsrc(uniform_ptr(a.dst + (cs + t0 * E) * sizeof(T))), lane * (uint32_t) sizeof(I), x);
+            }
+        } else if (t0 == ((nI + kFaninBlock - 1) / kFaninBlock) * kFaninBlock) {
+            // The block just past the vector body: the chunk's < E leftover elements, if any.
+            const uint64_t tail = (ce - cs) - nI * E;
+            if (lane < tail)
+                ((T *) (a.dst + (cs + nI * E) * sizeof(T)))[lane] =
+                    cload<T>(make_rsrc(uniform_ptr(rowbase + nI * E * sizeof(T))), lane * (uint32_t) sizeof(T));
+        }
+    }
+}
+
 // xGMI measurement hook (bench.py xgmi_probe): the same one-wave, one-item-per-thread shape as
 // fanin_kernel, but every source load carries an explicit cache policy so the probe compares
 // the collectives' system-coherent pulls (AUX = sc0 sc1) with nontemporal ones (AUX = nt) over
@@ -432,6 +500,51 @@ hipError_t scan_t(const ScanArgs &a, bool vec, int grid, hipStream_t s)
     if (a.p == 4) return launch_res(scan_kernel<T, true, 4>, a, grid, s);
     if (a.p == 8) return launch_res(scan_kernel<T, true, 8>, a, grid, s);
     return launch_res(scan_kernel<T, true, 0>, a, grid, s);
+}
+
+template <typename T>
+hipError_t scan_phase_t(const ScanArgs &a, bool vec, int phase, hipStream_t s)
+{
+    const uint64_t E = vec ? 16 / sizeof(T) : 1;
+    const uint64_t items = (a.items_per_chunk + E - 1) / E;
+    if (phase == 1) {
+        const uint64_t cs = std::min((uint64_t) a.me * a.items_per_chunk, a.nelems);
+        const uint64_t len = std::min(cs + a.items_per_chunk, a.nelems) - cs;
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((len / E + kFaninBlock - 1) / kFaninBlock,
+                                                                    (uint64_t) kFaninMaxGrid));
+        auto go = [&](auto kernel) { hipLaunchKernelGGL(kernel, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a); };
+        if (vec) {
+            if (a.p == 2) go(scan_p1_kernel<T, true, 2>);
+            else if (a.p == 4) go(scan_p1_kernel<T, true, 4>);
+            else if (a.p == 8) go(scan_p1_kernel<T, true, 8>);
+            else go(scan_p1_kernel<T, true, 0>);
+        } else {
+            if (a.p == 2) go(scan_p1_kernel<T, false, 2>);
+            else if (a.p == 4) go(scan_p1_kernel<T, false, 4>);
+            else if (a.p == 8) go(scan_p1_kernel<T, false, 8>);
+            else go(scan_p1_kernel<T, false, 0>);
+        }
+    } else {
+        // Blocks per chunk, plus one for the last chunk's < E leftover elements.
+        const uint64_t blocks = (items + kFaninBlock - 1) / kFaninBlock + 1;
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t) a.p * blocks, (uint64_t) kFaninMaxGrid));
+        if (vec) hipLaunchKernelGGL((scan_p2_kernel<T, true>), dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
+        else hipLaunchKernelGGL((scan_p2_kernel<T, false>), dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_phase(int dt, const ScanArgs &a, bool vec, int phase, hipStream_t s)
+{
+    switch (dt) {
+        case ISHMEMI_DT_INT8: case ISHMEMI_DT_UINT8: return scan_phase_t<uint8_t>(a, vec, phase, s);
+        case ISHMEMI_DT_INT16: case ISHMEMI_DT_UINT16: return scan_phase_t<uint16_t>(a, vec, phase, s);
+        case ISHMEMI_DT_INT32: case ISHMEMI_DT_UINT32: return scan_phase_t<uint32_t>(a, vec, phase, s);
+        case ISHMEMI_DT_INT64: case ISHMEMI_DT_UINT64: return scan_phase_t<uint64_t>(a, vec, phase, s);
+        case ISHMEMI_DT_FLOAT: return scan_phase_t<float>(a, vec, phase, s);
+        case ISHMEMI_DT_DOUBLE: return scan_phase_t<double>(a, vec, phase, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_scan(int dt, const ScanArgs &a, bool vec, int grid, hipStream_t s)

@@ -941,6 +941,19 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
             a.items_per_chunk = items_per_chunk(m, t.size);
             a.inclusive = inclusive;
             const bool vec = (((uintptr_t) dst | (uintptr_t) src | (uintptr_t) s.staging) & 15) == 0;
+            if ((long long) (m * es) >= s.phased_min) {
+                // Large segment: barrier, one-shot fold grid, barrier, one-shot pull grid, barrier
+                // (kernels_coll.hip scan_p1_kernel / scan_p2_kernel).  Every member knows m.
+                ReduceArgs r;
+                if (team_args(s, team, r, why)) return fail("scan: " + why);
+                r.ret = ret;
+                HIP_TRY(launch_team_sync(r, st));
+                HIP_TRY(launch_scan_phase(dt, a, vec, 1, st));
+                HIP_TRY(launch_team_sync(r, st));
+                HIP_TRY(launch_scan_phase(dt, a, vec, 2, st));
+                HIP_TRY(launch_team_sync(r, st));
+                continue;
+            }
             const uint64_t tile = (uint64_t) kBlock * 2 * (vec ? 16 / es : 1);
             const int grid = (int) std::max<uint64_t>(
                 1, std::min<uint64_t>((a.items_per_chunk + tile - 1) / tile, s.max_blocks));

@@ -50,6 +50,18 @@ for s in $STEPS; do
       done
     done
     unset ISHMEM_PHASED_MIN_BYTES ISHMEM_BENCH_SAME_DEVICE ;;
+  scansweep)
+    export ISHMEM_BENCH_SAME_DEVICE=1
+    for np_ in 2 8; do
+      for v in base phased; do
+        if [ $v = phased ]; then export ISHMEM_PHASED_MIN_BYTES=0; else export ISHMEM_PHASED_MIN_BYTES=-1; fi
+        timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np_ --master-addr 127.0.0.1 \
+          --master-port 2963$np_ tools/sweep.py --coll inscan --max-mib 256 --min-bytes 1048576 --factor 4 --iters 20 \
+          > $OUT/scan_${v}_p$np_.csv 2> $OUT/scan_${v}_p$np_.err || exit $?
+        echo "== inscan $v p$np_"; grep -v Gloo $OUT/scan_${v}_p$np_.csv
+      done
+    done
+    unset ISHMEM_PHASED_MIN_BYTES ISHMEM_BENCH_SAME_DEVICE ;;
   sweep)
     export ISHMEM_BENCH_SAME_DEVICE=1
     for np_ in 2 8; do
