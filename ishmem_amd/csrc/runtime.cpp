@@ -97,6 +97,10 @@ constexpr long long kPhasedOff = std::numeric_limits<long long>::max();
 // 0.99-1.13 ms persistent, 128 MiB 110 vs 145 us; below 64 MiB the two extra barrier round trips
 // cost more than the one-shot grids save.
 constexpr long long kPhasedDefault = 128ll << 20;
+// ...unless more PEs than this share one GPU (rehearsals only): the phased path's three barriers
+// are separate launches, and when eight processes time-slice one GPU each costs ~40-80 us
+// (8 PEs x 1 GiB: 3.94 vs 3.88 ms; scan 1817 vs 1606 us).  A PE that sets the variable keeps it.
+constexpr int kPhasedMaxShare = 4;
 
 struct PeRecord {
     int32_t pe, pid, device, flags_kind;
@@ -106,6 +110,7 @@ struct PeRecord {
     // Launch-shape parameters: the multi-PE kernels pair workgroup b with workgroup b of every
     // peer and choose the LL path per call, so every PE must use the same values.
     int64_t max_blocks, ll_max_bytes, oneshot_p2, phased_min;
+    int32_t phased_explicit;  // ISHMEM_PHASED_MIN_BYTES was set for this PE
     uint64_t staging_bytes;
     int64_t staging_slots;
     hipIpcMemHandle_t heap_handle;
@@ -1189,6 +1194,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.ll_max_bytes = s.ll_max_bytes;
         mine.oneshot_p2 = s.oneshot_p2;
         mine.phased_min = s.phased_min;
+        mine.phased_explicit = getenv("ISHMEM_PHASED_MIN_BYTES") && *getenv("ISHMEM_PHASED_MIN_BYTES");
         mine.staging_bytes = s.staging_bytes;
         mine.staging_slots = s.staging_slots;
         if (hipDeviceGetPCIBusId(mine.pci_bus, sizeof(mine.pci_bus), s.device) != hipSuccess) {
@@ -1219,6 +1225,16 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         bool coarse_forced = false;  // a test asked for coarse-grained flags (ISHMEM_FLAGS_KIND=2)
         for (int j = 0; j < npes; ++j) coarse_forced = coarse_forced || all[j].flags_kind_requested == kFlagsCoarse;
         set_device_share(share);
+        // The phased default by topology, from records every PE holds (so every PE decides alike).
+        int max_share = 0;
+        bool phased_explicit = false;
+        for (int j = 0; j < npes; ++j) {
+            int sj = 0;
+            for (int k = 0; k < npes; ++k) sj += strncmp(all[j].pci_bus, all[k].pci_bus, sizeof(mine.pci_bus)) == 0;
+            max_share = std::max(max_share, sj);
+            phased_explicit = phased_explicit || all[j].phased_explicit;
+        }
+        if (!phased_explicit && max_share > kPhasedMaxShare) s.phased_min = kPhasedOff;
         for (int j = 0; j < npes; ++j) {
             if (j == pe) continue;
             if (all[j].heap_size != s.heap_size)

@@ -86,6 +86,13 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             if int(ish.get_param("flags_kind")) != want:
                 fails.append(f"pe{pe} flags_kind {ish.get_param('flags_kind')} != agreed {want}")
 
+        if "phasedparam" in scenarios:
+            # The phased threshold agreed at init: the maximum over the PEs, off by default when
+            # more than 4 PEs share a device unless some PE set ISHMEM_PHASED_MIN_BYTES.
+            want = int(os.environ["PHASED_WANT"])
+            if int(ish.get_param("phased_min_bytes")) != want:
+                fails.append(f"pe{pe} phased_min_bytes {ish.get_param('phased_min_bytes')} != agreed {want}")
+
         if "timeout" in scenarios:
             # Failure detection: PE 0 enters collectives PE 1 never joins.  Every device-side
             # spin is bounded, so the call returns nonzero with a diagnostic instead of hanging

@@ -95,6 +95,21 @@ def test_launch_parameters_agreed_at_init():
                  "ISHMEM_STAGING_SIZE": ["4M", "8M", "2M"]})
 
 
+@pytest.mark.parametrize("case", ["p2_default", "p8_default", "p8_one_pe_explicit", "p3_one_pe_off"])
+def test_phased_threshold_agreed_at_init(case):
+    # Every PE must take the same path (the phased path's barriers are separate launches): the
+    # threshold is the maximum over the PEs; by default 128 MiB, off when more than 4 PEs share a
+    # GPU (time-sliced barriers) unless a PE set ISHMEM_PHASED_MIN_BYTES; -1 on any PE disables it.
+    npes, env, want = {
+        "p2_default": (2, {}, 128 << 20),
+        "p8_default": (8, {}, -1),
+        "p8_one_pe_explicit": (8, {"ISHMEM_PHASED_MIN_BYTES": [str(64 << 20)] + [""] * 7}, 128 << 20),
+        "p3_one_pe_off": (3, {"ISHMEM_PHASED_MIN_BYTES": ["", "-1", ""]}, -1),
+    }[case]
+    env = {"ISHMEM_PHASED_MIN_BYTES": "", **env}  # unset unless the case sets it (an outer setting would leak in)
+    run_pes(npes, ["phasedparam", "edge"], env={**env, "PHASED_WANT": want, "ISHMEM_MAX_BLOCKS": 8}, timeout=200)
+
+
 def test_missing_member_times_out_with_error_instead_of_hanging():
     run_pes(2, ["timeout"], timeout=120)
 
