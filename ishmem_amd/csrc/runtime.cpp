@@ -93,10 +93,11 @@ struct Team {
 };
 
 constexpr long long kPhasedOff = std::numeric_limits<long long>::max();
-// Measured (profiles/r03/phased/): 2 PEs x 1 GiB 0.84 ms phased against
-// 0.99-1.13 ms persistent, 128 MiB 110 vs 145 us; below 64 MiB the two extra barrier round trips
-// cost more than the one-shot grids save.
-constexpr long long kPhasedDefault = 128ll << 20;
+// Measured (profiles/r03/phased/, profiles/r03/paths/): 2 PEs x 1 GiB 0.84 ms phased
+// against 0.99-1.13 ms persistent; 2 PEs x 32 / 64 MiB 36 / 59 us against the two-member one-shot
+// fold's 42 / 78 us; 4 PEs x 16 MiB 40 vs 48 us; at 8 MiB and below the extra barrier round trips
+// cost what the one-shot grids save.
+constexpr long long kPhasedDefault = 16ll << 20;
 // ...unless more PEs than this share one GPU (rehearsals only): the phased path's three barriers
 // are separate launches, and when eight processes time-slice one GPU each costs ~40-80 us
 // (8 PEs x 1 GiB: 3.94 vs 3.88 ms; scan 1817 vs 1606 us).  A PE that sets the variable keeps it.
@@ -533,15 +534,10 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     // Not in place (a member would overwrite its source while the peer still reads it).  The
     // choice depends only on symmetric-address properties, so every member makes the same one.
     const uintptr_t d0 = (uintptr_t) dst, s0 = (uintptr_t) src, nb = n * es;
-    if (t.size == 2 && (long long) nb <= s.oneshot_p2 && (d0 + nb <= s0 || s0 + nb <= d0)) {
-        a.oneshot = 1;
-        a.items_per_chunk = pl.nitems;
-        a.seg_items = seg_items(pl.nitems);
-        pl.grid = (int) std::max<uint64_t>(
-            1, std::min<uint64_t>(nsegs(pl.nitems, a.seg_items), (uint64_t) s.max_blocks));
-    } else if (pl.vec && (long long) nb >= s.phased_min) {
-        // Large payloads: barrier, one-shot reduce-scatter, barrier, one-shot all-gather, barrier
-        // (kernels_impl.h, "Phased reduce-scatter + all-gather").  The barriers carry *ret.
+    if (pl.vec && (long long) nb >= s.phased_min) {
+        // From phased_min bytes: barrier, one-shot reduce-scatter, barrier, one-shot all-gather,
+        // barrier (kernels_impl.h, "Phased reduce-scatter + all-gather").  The barriers carry *ret.
+        // Checked before the two-member one-shot fold, which it beats from 32 MiB.
         PhaseArgs ph;
         memset(&ph, 0, sizeof(ph));
         for (int j = 0; j < t.size; ++j) {
@@ -562,6 +558,13 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         HIP_TRY(launch_ag_phase(ph, st));
         HIP_TRY(launch_team_sync(a, st));
         return 0;
+    }
+    if (t.size == 2 && (long long) nb <= s.oneshot_p2 && (d0 + nb <= s0 || s0 + nb <= d0)) {
+        a.oneshot = 1;
+        a.items_per_chunk = pl.nitems;
+        a.seg_items = seg_items(pl.nitems);
+        pl.grid = (int) std::max<uint64_t>(
+            1, std::min<uint64_t>(nsegs(pl.nitems, a.seg_items), (uint64_t) s.max_blocks));
     }
     HIP_TRY(launch_allreduce(op, dt, pl.vec, a, pl.grid, st));
     return 0;

@@ -98,12 +98,12 @@ def test_launch_parameters_agreed_at_init():
 @pytest.mark.parametrize("case", ["p2_default", "p8_default", "p8_one_pe_explicit", "p3_one_pe_off"])
 def test_phased_threshold_agreed_at_init(case):
     # Every PE must take the same path (the phased path's barriers are separate launches): the
-    # threshold is the maximum over the PEs; by default 128 MiB, off when more than 4 PEs share a
+    # threshold is the maximum over the PEs; by default 16 MiB, off when more than 4 PEs share a
     # GPU (time-sliced barriers) unless a PE set ISHMEM_PHASED_MIN_BYTES; -1 on any PE disables it.
     npes, env, want = {
-        "p2_default": (2, {}, 128 << 20),
+        "p2_default": (2, {}, 16 << 20),
         "p8_default": (8, {}, -1),
-        "p8_one_pe_explicit": (8, {"ISHMEM_PHASED_MIN_BYTES": [str(64 << 20)] + [""] * 7}, 128 << 20),
+        "p8_one_pe_explicit": (8, {"ISHMEM_PHASED_MIN_BYTES": [str(64 << 20)] + [""] * 7}, 64 << 20),
         "p3_one_pe_off": (3, {"ISHMEM_PHASED_MIN_BYTES": ["", "-1", ""]}, -1),
     }[case]
     env = {"ISHMEM_PHASED_MIN_BYTES": "", **env}  # unset unless the case sets it (an outer setting would leak in)
@@ -135,10 +135,12 @@ def test_eight_pes_collect_scan_team():
 
 
 def test_two_pe_reduce_scatter_allgather_path():
-    # At 2 PEs non-in-place reduces take the one-shot fold by default; force the RS + AG kernel
-    # (and no LL) for the same golden / offset / large cases.
+    # At 2 PEs non-in-place reduces take the one-shot fold (below 16 MiB) or the phased path by
+    # default; force the persistent RS + AG kernel (and no LL) for the same golden / offset /
+    # large cases.
     run_pes(2, ["golden", "offsets", "large"],
-            env={"ISHMEM_ONESHOT_P2_MAX_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_MAX_BLOCKS": 64})
+            env={"ISHMEM_ONESHOT_P2_MAX_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_MAX_BLOCKS": 64,
+                 "ISHMEM_PHASED_MIN_BYTES": -1})
 
 
 @pytest.mark.parametrize("npes", [2, 3, 4, 8])
@@ -177,10 +179,11 @@ def test_config4_eight_pes_1GiB_f32_sum_full_compare():
 @pytest.mark.parametrize("oneshot", ["default", "rs_ag"])
 def test_config3_two_pes_1GiB_f32_sum_full_compare(oneshot):
     # BASELINE configs[2]: 2 PEs x 1 GiB f32 sum, every word compared on both PEs (rotating-winner
-    # pattern); the default two-member kernel and forced reduce-scatter + all-gather.
+    # pattern); the default (phased) path and the persistent reduce-scatter + all-gather kernel.
     env = {"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "3G"}
     if oneshot == "rs_ag":
         env["ISHMEM_ONESHOT_P2_MAX_BYTES"] = 0
+        env["ISHMEM_PHASED_MIN_BYTES"] = -1
     run_pes(2, ["cfg3"], env=env, timeout=400)
 
 
