@@ -105,6 +105,17 @@ struct alignas(16) Vec16 {
     T e[16 / sizeof(T)];
 };
 constexpr int kUnroll = 4;  // 16-B items in flight per thread and member
+// The group's reduce-scatter loads this many members' items before folding them (a run-time loop
+// over members would wait for each member's loads before issuing the next member's: 4 x 16 B per
+// thread in flight), and the all-gather pulls this many 16-B items per thread per step.
+#ifndef ISHMEMX_DEV_MEMBER_BATCH
+#define ISHMEMX_DEV_MEMBER_BATCH 4
+#endif
+#ifndef ISHMEMX_DEV_AG_UNROLL
+#define ISHMEMX_DEV_AG_UNROLL 8
+#endif
+constexpr int kMemberBatch = ISHMEMX_DEV_MEMBER_BATCH;
+constexpr int kAgUnroll = ISHMEMX_DEV_AG_UNROLL;
 
 template <typename T, int OP>
 __device__ __forceinline__ Vec16<T> op16(const Vec16<T> &a, const Vec16<T> &b)
@@ -267,18 +278,27 @@ __device__ int reduce_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, 
     const size_t nv = vec ? (ce - cs) / E : 0;
     for (size_t v0 = 0; v0 < nv; v0 += (size_t) nthr * kUnroll) {
         Vec16<T> acc[kUnroll];
-        for (int j = 0; j < size; ++j) {
-            const int gpe = start + j * stride;
-            const char *base = (j == me) ? (const char *) (source + cs) : peer_addr(c, source + cs, gpe);
-            const char *step = group_uniform(base + v0 * 16);
-            Vec16<T> x[kUnroll];
+        for (int j0 = 0; j0 < size; j0 += kMemberBatch) {
+            Vec16<T> x[kMemberBatch][kUnroll];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const size_t k = (size_t) u * nthr + tid;
-                if (v0 + k < nv) x[u] = sys_load16<T>(step, (uint32_t) (k * 16));
+            for (int b = 0; b < kMemberBatch; ++b) {
+                const int j = j0 + b;
+                if (j >= size) break;
+                const int gpe = start + j * stride;
+                const char *base = (j == me) ? (const char *) (source + cs) : peer_addr(c, source + cs, gpe);
+                const char *step = group_uniform(base + v0 * 16);
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    const size_t k = (size_t) u * nthr + tid;
+                    if (v0 + k < nv) x[b][u] = sys_load16<T>(step, (uint32_t) (k * 16));
+                }
             }
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) acc[u] = (j == 0) ? x[u] : op16<T, OP>(acc[u], x[u]);
+            for (int b = 0; b < kMemberBatch; ++b) {
+                if (j0 + b >= size) break;
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) acc[u] = (j0 + b == 0) ? x[b][u] : op16<T, OP>(acc[u], x[b][u]);
+            }
         }
         char *dstep = (char *) group_uniform((const char *) (dest + cs) + v0 * 16);
 #pragma unroll
@@ -304,17 +324,17 @@ __device__ int reduce_group(const ishmemi_c_device_ctx_t *c, int team, T *dest, 
         const size_t je = js + per < nreduce ? js + per : nreduce;
         const size_t jv = vec ? (je - js) / E : 0;
         const char *pbase = peer_addr(c, dest + js, gpe);
-        for (size_t v0 = 0; v0 < jv; v0 += (size_t) nthr * kUnroll) {
+        for (size_t v0 = 0; v0 < jv; v0 += (size_t) nthr * kAgUnroll) {
             const char *step = group_uniform(pbase + v0 * 16);
-            Vec16<T> x[kUnroll];
+            Vec16<T> x[kAgUnroll];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
+            for (int u = 0; u < kAgUnroll; ++u) {
                 const size_t q = (size_t) u * nthr + tid;
                 if (v0 + q < jv) x[u] = sys_load16<T>(step, (uint32_t) (q * 16));
             }
             Vec16<T> *dp = (Vec16<T> *) (dest + js) + v0;
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
+            for (int u = 0; u < kAgUnroll; ++u) {
                 const size_t q = (size_t) u * nthr + tid;
                 if (v0 + q < jv) dp[q] = x[u];
             }

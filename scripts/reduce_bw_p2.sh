@@ -5,9 +5,9 @@ set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 KEY="bw$$"
 export HSA_ENABLE_IPC_MODE_LEGACY=0 ISHMEM_NPES=2 ISHMEM_DEVICE=0 ISHMEM_BOOTSTRAP_KEY=$KEY ISHMEM_MAX_BLOCKS=${MB:-128}
-ISHMEM_PE=1 timeout -k 10 500 "$R/build/reduce_bw" --csv -m "$1" > /dev/null 2>&1 &
+ISHMEM_PE=1 timeout -k 10 500 "${EXE:-$R/build/reduce_bw}" --csv -m "$1" > /dev/null 2>&1 &
 P1=$!
-ISHMEM_PE=0 timeout -k 10 500 "$R/build/reduce_bw" --csv -m "$1" > "$2" 2>&1
+ISHMEM_PE=0 timeout -k 10 500 "${EXE:-$R/build/reduce_bw}" --csv -m "$1" > "$2" 2>&1
 RC=$?
 wait $P1
 RC1=$?
