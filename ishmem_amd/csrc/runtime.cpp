@@ -85,6 +85,20 @@ long long env_ll(const char *name, long long dflt)
     return (s && *s) ? atoll(s) : dflt;
 }
 
+// A byte-count variable: plain bytes or with a K / M / G suffix ("16M"), 0 allowed, negative = -1.
+long long env_bytes(const char *name, long long dflt)
+{
+    const char *s = getenv(name);
+    if (!s || !*s) return dflt;
+    char *end = nullptr;
+    double v = strtod(s, &end);
+    if (end == s) return dflt;
+    if (*end == 'k' || *end == 'K') v *= 1024.0;
+    else if (*end == 'm' || *end == 'M') v *= 1024.0 * 1024.0;
+    else if (*end == 'g' || *end == 'G') v *= 1024.0 * 1024.0 * 1024.0;
+    return v < 0 ? -1 : (long long) v;
+}
+
 struct Team {
     bool valid = false;
     int start = 0, stride = 1, size = 1;  // in world PEs (src/teams.h:56-76)
@@ -1133,12 +1147,12 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, env_ll("ISHMEM_MAX_BLOCKS", kMaxBlocks)));
     s.timeout_ms = std::max<long long>(1, env_ll("ISHMEM_TIMEOUT_MS", 60000));
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
-                                         std::max<long long>(0, env_ll("ISHMEM_LL_MAX_BYTES", (long long) kLLDefaultBytes)));
+                                         std::max<long long>(0, env_bytes("ISHMEM_LL_MAX_BYTES", (long long) kLLDefaultBytes)));
     s.debug = (int) env_ll("ISHMEM_DEBUG", 0);
     s.trace = nullptr;
     s.stream_order = env_ll("ISHMEM_STREAM_ORDER", 0) != 0;
-    s.oneshot_p2 = std::max<long long>(0, env_ll("ISHMEM_ONESHOT_P2_MAX_BYTES", 64ll << 20));
-    s.phased_min = env_ll("ISHMEM_PHASED_MIN_BYTES", kPhasedDefault);
+    s.oneshot_p2 = std::max<long long>(0, env_bytes("ISHMEM_ONESHOT_P2_MAX_BYTES", 64ll << 20));
+    s.phased_min = env_bytes("ISHMEM_PHASED_MIN_BYTES", kPhasedDefault);
     if (s.phased_min < 0) s.phased_min = kPhasedOff;
     s.staging_bytes = (parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20) + kHeapAlign - 1) &
                       ~(size_t) (kHeapAlign - 1);

@@ -103,7 +103,7 @@ def test_phased_threshold_agreed_at_init(case):
     npes, env, want = {
         "p2_default": (2, {}, 16 << 20),
         "p8_default": (8, {}, -1),
-        "p8_one_pe_explicit": (8, {"ISHMEM_PHASED_MIN_BYTES": [str(64 << 20)] + [""] * 7}, 64 << 20),
+        "p8_one_pe_explicit": (8, {"ISHMEM_PHASED_MIN_BYTES": ["64M"] + [""] * 7}, 64 << 20),  # K / M / G suffixes
         "p3_one_pe_off": (3, {"ISHMEM_PHASED_MIN_BYTES": ["", "-1", ""]}, -1),
     }[case]
     env = {"ISHMEM_PHASED_MIN_BYTES": "", **env}  # unset unless the case sets it (an outer setting would leak in)
