@@ -57,7 +57,8 @@ def main() -> None:
                         "write_size_kb": wk, "hbm_bytes_per_launch": hbm,
                         "algorithmic_bytes_per_launch": mult * payload,
                         "traffic_over_algorithmic": hbm / (mult * payload),
-                        "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streams)", "source": tag}
+                        "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streams)",
+                        "source": f"profiles/{tag}_pmc_{{fetch,write}}_size.csv"}
     summary_path.write_text(json.dumps(summary, indent=2) + "\n")
     print(json.dumps(summary, indent=2))
 
