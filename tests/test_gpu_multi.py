@@ -156,11 +156,16 @@ def test_phased_reduce_scatter_allgather_path(npes):
             timeout=400)
 
 
-def test_reduce_completes_while_another_kernel_holds_most_cus():
+@pytest.mark.parametrize("path", ["phased", "persistent"])
+def test_reduce_completes_while_another_kernel_holds_most_cus(path):
     # Weakness of the round-1 protocol (workgroup b of every PE paired with workgroup b of every
     # peer): a collective whose partner workgroups cannot all be resident.  Now any workgroup may
-    # satisfy a start flag and work is grabbed, so the reduce runs on whatever CUs are free.
-    run_pes(2, ["occupied"], env={"ISHMEM_MAX_BLOCKS": 1024}, timeout=120)
+    # satisfy a start flag and work is grabbed (persistent kernel), or no grid waits at all
+    # (phased path: only its one-workgroup barriers do), so the reduce runs on whatever CUs are free.
+    env = {"ISHMEM_MAX_BLOCKS": 1024}
+    if path == "persistent":
+        env["ISHMEM_PHASED_MIN_BYTES"] = -1
+    run_pes(2, ["occupied"], env=env, timeout=120)
 
 
 @pytest.mark.parametrize("npes", [2, 4, 8])
