@@ -255,8 +255,8 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     MI355X per PE cannot be rehearsed on a one-GPU box):
       grid  - the payload with the workgroup cap at 128 / 256 / 512 / 1024 (then clamped to the
               resident capacity);
-      phased - the payload on the phased path (one-shot grids between barriers) and on the
-               persistent kernel;
+      phased - 4 / 16 / 64 MiB and the payload on the phased path (one-shot grids between
+               barriers) and on the persistent kernel (the phased threshold);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
       ll    - 4 / 16 / 64 KiB with the one-hop granule path on (default) and off."""
 
@@ -294,8 +294,10 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     for mb in (128, 256, 512, 1024):
         if mb <= cap:
             run("grid", "max_blocks", mb, B, 5)
-    run("phased", "phased_min_bytes", 0, B, 5)
-    run("persistent", "phased_min_bytes", -1, B, 5)
+    for nb in sorted({4 << 20, 16 << 20, 64 << 20, B}):
+        if nb <= B:
+            run("phased", "phased_min_bytes", 0, nb, 5 if nb == B else 20)
+            run("persistent", "phased_min_bytes", -1, nb, 5 if nb == B else 20)
     if world == 2:
         run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
         run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)
