@@ -147,6 +147,9 @@ hipError_t launch_scan(int dt, const ScanArgs &a, bool vec, int grid, hipStream_
 // Phased scan: phase 1 (fold chunk me into this PE's scratch rows) or 2 (pull this PE's rows),
 // one-shot grids, to be separated by launch_team_sync on the same stream.
 hipError_t launch_scan_phase(int dt, const ScanArgs &a, bool vec, int phase, hipStream_t s);
+// Direct two-member scan (no scratch): one-shot fold of members 0..me into dest, between team
+// barriers launched by the caller.
+hipError_t launch_scan_direct(int dt, const ScanArgs &a, bool vec, hipStream_t s);
 
 // Arguments of the local k-input fan-in combine: dst = op(src0, src1, ..., src_{k-1}).
 constexpr int kMaxFanin = 16;

@@ -373,6 +373,54 @@ __global__ __launch_bounds__(kFaninBlock) void scan_p2_kernel(ScanArgs a, uint64
     }
 }
 
+// Direct scan (runtime.cpp scan_impl: two members, disjoint dest and source, >= the phased
+// threshold): between two team barriers, member me folds members 0..me (inclusive) or 0..me-1
+// (exclusive; member 0 gets zeros) straight into its dest — no scratch rows, no second grid.
+// Member me pulls me * B over the links, so for two members this equals the two-phase scan's
+// ingress (B) with less HBM traffic; for more members the last one would pull (p-1) * B.
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kFaninBlock) void scan_direct_kernel(ScanArgs a)
+{
+    using I = std::conditional_t<VEC, Vec<T>, T>;
+    constexpr uint64_t E = sizeof(I) / sizeof(T);
+    const int me = a.me;
+    const int last = a.inclusive ? me : me - 1;  // fold members 0..last (none when last < 0)
+    const uint64_t nI = a.nelems / E, tail = a.nelems - nI * E;
+    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
+    const uint32_t lane = threadIdx.x, off = lane * (uint32_t) sizeof(I);
+    for (uint64_t t0 = (uint64_t) blockIdx.x * kFaninBlock; t0 < nI; t0 += stride) {
+        if (t0 + lane >= nI) continue;
+        const uint64_t wb = t0 * E * sizeof(T);
+        I acc{};
+        for (int j = 0; j <= last; ++j) {
+            const I x = j == me ? *(const I *) (a.src[j] + wb + off) : cload<I>(make_rsrc(uniform_ptr(a.src[j] + wb)), off);
+            acc = j == 0 ? x : scan_add<T, I>(acc, x);  // first term kept (sign of zero)
+        }
+        wt_store(make_rsrc(uniform_ptr(a.dst + wb)), off, acc);
+    }
+    if (blockIdx.x == 0 && lane < tail) {
+        const uint64_t rb = nI * E * sizeof(T);
+        const uint32_t eo = lane * (uint32_t) sizeof(T);
+        T acc{};
+        for (int j = 0; j <= last; ++j) {
+            const T x = j == me ? ((const T *) (a.src[j] + rb))[lane] : cload<T>(make_rsrc(uniform_ptr(a.src[j] + rb)), eo);
+            acc = j == 0 ? x : scan_add<T, T>(acc, x);
+        }
+        wt_store(make_rsrc(uniform_ptr(a.dst + rb)), eo, acc);
+    }
+}
+
+template <typename T>
+hipError_t scan_direct_t(const ScanArgs &a, bool vec, hipStream_t s)
+{
+    const uint64_t E = vec ? 16 / sizeof(T) : 1;
+    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((a.nelems / E + kFaninBlock - 1) / kFaninBlock,
+                                                                (uint64_t) kFaninMaxGrid));
+    if (vec) hipLaunchKernelGGL((scan_direct_kernel<T, true>), dim3((unsigned) g), dim3(kFaninBlock), 0, s, a);
+    else hipLaunchKernelGGL((scan_direct_kernel<T, false>), dim3((unsigned) g), dim3(kFaninBlock), 0, s, a);
+    return hipGetLastError();
+}
+
 // xGMI measurement hook (bench.py xgmi_probe): the same one-wave, one-item-per-thread shape as
 // fanin_kernel, but every source load carries an explicit cache policy so the probe compares
 // the collectives' system-coherent pulls (AUX = sc0 sc1) with nontemporal ones (AUX = nt) over
@@ -532,6 +580,19 @@ hipError_t scan_phase_t(const ScanArgs &a, bool vec, int phase, hipStream_t s)
         else hipLaunchKernelGGL((scan_p2_kernel<T, false>), dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
     }
     return hipGetLastError();
+}
+
+hipError_t launch_scan_direct(int dt, const ScanArgs &a, bool vec, hipStream_t s)
+{
+    switch (dt) {
+        case ISHMEMI_DT_INT8: case ISHMEMI_DT_UINT8: return scan_direct_t<uint8_t>(a, vec, s);
+        case ISHMEMI_DT_INT16: case ISHMEMI_DT_UINT16: return scan_direct_t<uint16_t>(a, vec, s);
+        case ISHMEMI_DT_INT32: case ISHMEMI_DT_UINT32: return scan_direct_t<uint32_t>(a, vec, s);
+        case ISHMEMI_DT_INT64: case ISHMEMI_DT_UINT64: return scan_direct_t<uint64_t>(a, vec, s);
+        case ISHMEMI_DT_FLOAT: return scan_direct_t<float>(a, vec, s);
+        case ISHMEMI_DT_DOUBLE: return scan_direct_t<double>(a, vec, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_scan_phase(int dt, const ScanArgs &a, bool vec, int phase, hipStream_t s)

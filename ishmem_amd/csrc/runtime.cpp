@@ -945,6 +945,35 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
         const uint64_t ipc_max = ((s.staging_bytes / es) / (uint64_t) t.size) & ~uint64_t(63);
         const uint64_t seg = ipc_max * (uint64_t) t.size;
         if (ipc_max == 0) return fail("scan: staging region too small for this team");
+        const uintptr_t d0 = (uintptr_t) dst, s0 = (uintptr_t) src, nb = n * es;
+        if (t.size == 2 && (long long) nb >= s.phased_min && (d0 + nb <= s0 || s0 + nb <= d0)) {
+            // Two members, disjoint buffers: barrier, direct one-shot fold, barrier (no scratch;
+            // kernels_coll.hip scan_direct_kernel).  Every member sees the same n and the same
+            // symmetric offsets, so all take this path together.
+            if (order_stream(s, st)) return 1;
+            ScanArgs a;
+            memset(&a, 0, sizeof(a));
+            std::string why;
+            if (fill_team_sync_args(s, team, a, why)) return fail("scan: " + why);
+            for (int j = 0; j < t.size; ++j) a.src[j] = translate(s, src, t.start + j * t.stride);
+            a.dst = (char *) dst;
+            a.ret = ret;
+            a.nelems = n;
+            a.inclusive = inclusive;
+            ReduceArgs r;
+            if (team_args(s, team, r, why)) return fail("scan: " + why);
+            r.ret = ret;
+            const bool vec = ((d0 | s0) & 15) == 0;
+            HIP_TRY(launch_team_sync(r, st));
+            HIP_TRY(launch_scan_direct(dt, a, vec, st));
+            HIP_TRY(launch_team_sync(r, st));
+            if (mark_stream(s, st)) return 1;
+            if (blocking) {
+                HIP_TRY(hipStreamSynchronize(st));
+                if (check_team_errors(s, team)) return 1;
+            }
+            return 0;
+        }
         if (order_stream(s, st) || staging_acquire(s, st)) return 1;
         for (uint64_t off = 0; off < n; off += seg) {
             const uint64_t m = std::min<uint64_t>(seg, n - off);

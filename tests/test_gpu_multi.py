@@ -86,6 +86,15 @@ def test_fcollect_collect_scan_vs_tester_patterns_and_oracle(npes):
     run_pes(npes, ["collect", "scan"], env={"ISHMEM_STAGING_SIZE": "4M"}, timeout=300)
 
 
+@pytest.mark.parametrize("npes", [2, 3])
+def test_scan_collect_on_the_phased_paths(npes):
+    # The threshold forced to 0: at 2 PEs disjoint scans take the direct fold (no scratch), in-place
+    # ones and every scan at 3 PEs the phased segments; fcollect / collect the phased pull grid.
+    # Tester patterns and seeded inputs vs the oracle, as in the default-path test above.
+    run_pes(npes, ["collect", "scan"], env={"ISHMEM_STAGING_SIZE": "4M", "ISHMEM_PHASED_MIN_BYTES": 0},
+            timeout=300)
+
+
 def test_launch_parameters_agreed_at_init():
     # Per-PE environments that disagree on the grid cap, the LL threshold and the staging size:
     # init takes the minimum, so the collectives still pair up (a mismatch would otherwise split
