@@ -165,6 +165,14 @@ def test_phased_reduce_scatter_allgather_path(npes):
             timeout=400)
 
 
+@pytest.mark.parametrize("npes,scenarios", [(4, ["team", "stream", "streams", "staged"]), (6, ["teams2"])])
+def test_phased_paths_on_teams_streams_and_staged_buffers(npes, scenarios):
+    # The phased paths forced, on strided / nested / 2-D teams, the reference's negative-stride,
+    # translate and shared team tests, on-stream calls with *ret and host / non-heap buffers
+    # through the staging pipeline.
+    run_pes(npes, scenarios, env={"ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_MAX_BLOCKS": 16}, timeout=300)
+
+
 @pytest.mark.parametrize("path", ["phased", "persistent"])
 def test_reduce_completes_while_another_kernel_holds_most_cus(path):
     # Weakness of the round-1 protocol (workgroup b of every PE paired with workgroup b of every
