@@ -182,9 +182,12 @@ template <typename A>
 __device__ __forceinline__ void kernel_epoch_done(const A &a, uint32_t ep)
 {
     __shared__ int s_last;
+    // A one-workgroup grid (the team barrier, which the phased paths launch three times per call)
+    // is its own last workgroup: no returning atomic on its critical path.
     if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(a.ep_ctr + kEpDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 gridDim.x - 1;
+        s_last = gridDim.x == 1 ||
+                 __hip_atomic_fetch_add(a.ep_ctr + kEpDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     gridDim.x - 1;
     __syncthreads();
     if (s_last && threadIdx.x < 64) {
         // Every launch word back to zero, the failure word included (a timed-out team sync must
