@@ -173,6 +173,22 @@ def test_phased_paths_on_teams_streams_and_staged_buffers(npes, scenarios):
     run_pes(npes, scenarios, env={"ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_MAX_BLOCKS": 16}, timeout=300)
 
 
+@pytest.mark.parametrize("npes", [2, 8])
+def test_one_pe_per_gpu_configuration_emulated(npes):
+    # The 8-GPU node's path choices, rehearsed on the one GPU: every PE reports its own device
+    # (ISHMEM_TEST_PCI_BUS), so the device share is 1 and the phased default is on at every team
+    # size (16 MiB), while the PEs still share one GPU.  Golden inputs, in place, edges, 256 / 64 MiB
+    # in full, hipGraph replay and the tripwire must all hold.  The grid cap keeps all PEs' grids
+    # resident together: with share 1 each PE would size its persistent grid for the whole GPU, and
+    # eight such grids on one device let one PE's waiting workgroups hold every CU a peer needs to
+    # announce (measured: device timeouts in the tripwire) — the co-location hazard the share-based
+    # split prevents, which one PE per GPU cannot meet.
+    env = {"ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 768 // npes,
+           "ISHMEM_PHASED_MIN_BYTES": "", "PHASED_WANT": 16 << 20}
+    run_pes(npes, ["phasedparam", "golden", "inplace", "edge", "large", "graph", "tripwire"], env=env,
+            timeout=400)
+
+
 @pytest.mark.parametrize("path", ["phased", "persistent"])
 def test_reduce_completes_while_another_kernel_holds_most_cus(path):
     # Weakness of the round-1 protocol (workgroup b of every PE paired with workgroup b of every
