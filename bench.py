@@ -170,6 +170,39 @@ def roofline(world: int, share: int, B: int, kern_ms: float, kernel: str = "allr
     return roof, t_roof
 
 
+def phase_breakdown(ish, B: int, world: int, share: int, dist, step, barrier) -> dict:
+    """One more call of the timed step with HIP events between the phased path's five launches
+    (set_param "phase_events", ishmemi_c_phase_times): start barrier, reduce-scatter grid, middle
+    barrier, all-gather grid, end barrier, each the max over ranks.  Per-PE link ingress of each
+    grid is (p - 1)/p * B; on one GPU (share > 1) the device's HBM traffic of the co-located PEs
+    is share * (1 + 1/p) * B for the reduce-scatter and share * 2 (p - 1)/p * B for the
+    all-gather."""
+    import ctypes
+    L = ish.lib()
+    ish.set_param("phase_events", 1)
+    try:
+        barrier()
+        step()
+        ms = (ctypes.c_float * 5)()
+        if L.ishmemi_c_phase_times(ms) != 0:
+            raise RuntimeError(ish.last_error())
+        barrier()
+    finally:
+        ish.set_param("phase_events", 0)
+    t = max_over_ranks(dist, [float(x) for x in ms])
+    names = ["start_barrier", "reduce_scatter", "mid_barrier", "all_gather", "end_barrier"]
+    out = {"ms": dict(zip(names, t))}
+    ingress = (world - 1) / world * B
+    out["ingress_GBps_per_pe"] = {"reduce_scatter": ingress / (t[1] * 1e-3) / 1e9,
+                                  "all_gather": ingress / (t[3] * 1e-3) / 1e9}
+    if share > 1:
+        rs_dev = share * (1 + 1 / world) * B
+        ag_dev = share * 2 * (world - 1) / world * B
+        out["device_hbm_GBps"] = {"reduce_scatter": rs_dev / (t[1] * 1e-3) / 1e9,
+                                  "all_gather": ag_dev / (t[3] * 1e-3) / 1e9}
+    return out
+
+
 def max_over_ranks(dist, vals: list[float]) -> list[float]:
     if dist is None:
         return vals
@@ -768,6 +801,13 @@ def main() -> int:
                             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("combine2_1pe", B)}
         ish.ishmem_free(b2)
+
+    if world > 1 and healthy() and roof["kernel"].startswith("rs_phase"):
+        log("phase breakdown")
+        try:
+            extra["phases"] = phase_breakdown(ish, B, world, share, dist, step, barrier)
+        except Exception as ex:
+            extra["phases"] = {"error": str(ex)}
 
     if world > 1 and healthy() and not args.no_probe:
         log("xGMI probe")

@@ -260,7 +260,10 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
  * device-side spin), "stream_order" (1: collectives issued on different streams are ordered by
  * the library in call order, ~2 us per call; 0, the default: the caller orders them, as the
  * reference requires), "oneshot_p2_max_bytes" (two-member teams: one-phase fold up to this size,
- * default 64 MiB), "debug".  "ll_max_bytes" and "oneshot_p2_max_bytes" choose the kernel of a
+ * default 64 MiB), "phased_min_bytes" (payloads of at least this size take the phased path:
+ * barrier, one-shot reduce-scatter, barrier, one-shot all-gather, barrier; -1 disables it),
+ * "phase_events" (1: the next phased reduces record HIP events between their five launches, read
+ * with ishmemi_c_phase_times; a measurement hook), "debug".  "ll_max_bytes" and "oneshot_p2_max_bytes" choose the kernel of a
  * multi-PE call: init agrees on them (minimum over the PEs) and a later set_param must be made
  * with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,
  * nothing is paired by workgroup index).  ishmemi_c_get_param also reports "staging_bytes",
@@ -269,6 +272,10 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
 const char *ishmemi_c_last_error(void);
 int ishmemi_c_set_param(const char *name, long long value);
 long long ishmemi_c_get_param(const char *name);
+/* Durations (ms) of the last phased reduce's five launches — start barrier, reduce-scatter grid,
+ * middle barrier, all-gather grid, end barrier — recorded while set_param("phase_events", 1) is
+ * on.  Synchronises on the last event.  Returns 0, or nonzero if no phased reduce was recorded. */
+int ishmemi_c_phase_times(float *ms5);
 /* Number of collective launches whose device-side barriers timed out since init. */
 int ishmemi_c_error_count(void);
 /* Bytes of one element of `dtype` (0 if invalid); 1 if (op, dtype) is a valid pair. */

@@ -67,6 +67,7 @@ PROTOTYPES = [
     ("ishmemi_c_last_error", ctypes.c_char_p, []),
     ("ishmemi_c_set_param", _i, [ctypes.c_char_p, _ll]),
     ("ishmemi_c_get_param", _ll, [ctypes.c_char_p]),
+    ("ishmemi_c_phase_times", _i, [ctypes.POINTER(ctypes.c_float)]),
     ("ishmemi_c_error_count", _i, []),
     ("ishmemi_c_dtype_size", _sz, [_i]),
     ("ishmemi_c_op_dtype_valid", _i, [_i, _i]),

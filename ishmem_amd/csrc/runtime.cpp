@@ -186,6 +186,9 @@ struct State {
     int debug = 0;
     int error_count = 0;
     uint64_t *trace = nullptr;  // development phase-timestamp buffer (device memory)
+    // Measurement hook (set_param "phase_events"): events around the phased reduce's launches.
+    bool phase_events = false, phase_recorded = false;
+    hipEvent_t phase_ev[6] = {};
 };
 
 State &S()
@@ -566,11 +569,23 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         ph.elem = (uint32_t) es;
         ph.p = t.size;
         ph.me = t.my_idx;
+        const bool ev = s.phase_events && !capturing(st);
+        auto mark = [&](int k) -> int {
+            if (ev) HIP_TRY(hipEventRecord(s.phase_ev[k], st));
+            return 0;
+        };
+        if (mark(0)) return 1;
         HIP_TRY(launch_team_sync(a, st));
+        if (mark(1)) return 1;
         HIP_TRY(launch_rs_phase(op, dt, ph, st));
+        if (mark(2)) return 1;
         HIP_TRY(launch_team_sync(a, st));
+        if (mark(3)) return 1;
         HIP_TRY(launch_ag_phase(ph, st));
+        if (mark(4)) return 1;
         HIP_TRY(launch_team_sync(a, st));
+        if (mark(5)) return 1;
+        s.phase_recorded = s.phase_recorded || ev;
         return 0;
     }
     if (t.size == 2 && (long long) nb <= s.oneshot_p2 && (d0 + nb <= s0 || s0 + nb <= d0)) {
@@ -1477,6 +1492,12 @@ int ishmemi_c_finalize(void)
         }
         s.copy_in = s.copy_out = nullptr;
     }
+    if (s.phase_ev[0])
+        for (hipEvent_t &e : s.phase_ev) {
+            (void) hipEventDestroy(e);
+            e = nullptr;
+        }
+    s.phase_events = s.phase_recorded = false;
     (void) hipFree(s.heap);
     (void) hipFree(s.flags);
     (void) hipHostFree(s.err_host);
@@ -2137,6 +2158,16 @@ void *ishmemi_c_device_ctx(void)
 
 const char *ishmemi_c_last_error(void) { return g_last_error.c_str(); }
 
+int ishmemi_c_phase_times(float *ms5)
+{
+    State &s = S();
+    if (!ms5) return fail("phase_times: null output");
+    if (!s.phase_recorded || !s.phase_ev[0]) return fail("phase_times: no phased reduce recorded (set_param phase_events 1)");
+    HIP_TRY(hipEventSynchronize(s.phase_ev[5]));
+    for (int k = 0; k < 5; ++k) HIP_TRY(hipEventElapsedTime(&ms5[k], s.phase_ev[k], s.phase_ev[k + 1]));
+    return 0;
+}
+
 int ishmemi_c_set_param(const char *name, long long value)
 {
     State &s = S();
@@ -2150,6 +2181,11 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "ll_max_bytes") s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes, std::max<long long>(0, value));
     else if (n == "debug") s.debug = (int) value;
     else if (n == "trace_buffer") s.trace = (uint64_t *) (uintptr_t) value;
+    else if (n == "phase_events") {
+        if (value && !s.phase_ev[0])
+            for (hipEvent_t &e : s.phase_ev) HIP_TRY(hipEventCreate(&e));
+        s.phase_events = value != 0;
+    }
     else return fail("set_param: unknown parameter " + n);
     return 0;
 }
