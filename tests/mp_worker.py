@@ -86,6 +86,25 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             if int(ish.get_param("flags_kind")) != want:
                 fails.append(f"pe{pe} flags_kind {ish.get_param('flags_kind')} != agreed {want}")
 
+        if "phaseevents" in scenarios:
+            # The measurement hook: a phased reduce with events between its five launches.
+            import ctypes
+            n = 1 << 20
+            s_, d_ = heap(n, DT["float"]), heap(n, DT["float"])
+            hip.upload(s_, np.full(n, pe + 1, np.float32))
+            ms = (ctypes.c_float * 5)()
+            if ish.lib().ishmemi_c_phase_times(ms) == 0:
+                fails.append(f"pe{pe} phase_times succeeded before any phased reduce was recorded")
+            ish.set_param("phase_events", 1)
+            r = ish.ishmem_float_sum_reduce(d_, s_, n)
+            rc = ish.lib().ishmemi_c_phase_times(ms)
+            ish.set_param("phase_events", 0)
+            want = npes * (npes + 1) / 2
+            if r or rc or not all(x > 0 for x in ms) or not np.all(hip.download(d_, n, np.float32) == want):
+                fails.append(f"pe{pe} phaseevents: rc={r}/{rc} ms={list(ms)} {ish.last_error()}")
+            ish.ishmem_free(d_)
+            ish.ishmem_free(s_)
+
         if "phasedparam" in scenarios:
             # The phased threshold agreed at init: the maximum over the PEs, off by default when
             # more than 4 PEs share a device unless some PE set ISHMEM_PHASED_MIN_BYTES.

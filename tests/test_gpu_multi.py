@@ -159,7 +159,7 @@ def test_phased_reduce_scatter_allgather_path(npes):
     # the golden inputs (every op / type), in place, the offset sweep (head / tail elements, empty
     # chunks), edge cases, 256 MiB per PE compared in full, hipGraph replay and the chained-
     # producer coherence tripwire.  p = 3 runs the run-time team-size fold.
-    run_pes(npes, ["golden", "inplace", "offsets", "edge", "large", "graph", "tripwire"],
+    run_pes(npes, ["phaseevents", "golden", "inplace", "offsets", "edge", "large", "graph", "tripwire"],
             env={"ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_ONESHOT_P2_MAX_BYTES": 0,
                  "ISHMEM_MAX_BLOCKS": 64},
             timeout=400)
