@@ -263,9 +263,10 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
  * default 64 MiB), "phased_min_bytes" (payloads of at least this size take the phased path:
  * barrier, one-shot reduce-scatter, barrier, one-shot all-gather, barrier; -1 disables it),
  * "phase_events" (1: the next phased reduces record HIP events between their five launches, read
- * with ishmemi_c_phase_times; a measurement hook), "debug".  "ll_max_bytes" and "oneshot_p2_max_bytes" choose the kernel of a
- * multi-PE call: init agrees on them (minimum over the PEs) and a later set_param must be made
- * with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,
+ * with ishmemi_c_phase_times; a measurement hook), "debug".  "ll_max_bytes",
+ * "oneshot_p2_max_bytes" and "phased_min_bytes" choose the kernels of a multi-PE call: init
+ * agrees on them (the minimum over the PEs; the maximum for "phased_min_bytes") and a later
+ * set_param must be made with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,
  * nothing is paired by workgroup index).  ishmemi_c_get_param also reports "staging_bytes",
  * "heap_bytes", "flags_fine_grained", "cu_count" (compute units of this PE's device) and
  * "device_share" (PEs of the job on this PE's device: 1 with one PE per GPU). */
