@@ -21,6 +21,9 @@
 //     reference's results differ between PEs for FP, docs/source/collectives.rst:1241-1244) and
 //     equal to the reference's PE-0 result and to its tester's check pattern
 //     (test/unit/reduce_sum.cpp:203-224).
+//   * rs_phase_kernel / ag_phase_kernel: the same reduce-scatter + all-gather for large payloads
+//     as two one-shot grids (the fan-in kernel's shape) between one-workgroup team barriers —
+//     nothing in either grid waits, so it runs at the streaming kernels' rate (round 3).
 //   * The barriers replace ishmemi_team_sync's psync counters (src/collectives/sync_impl.h:30-69)
 //     with epoch-tagged flags in fine-grained memory: one "started" flag per member, one
 //     "ready" flag per reduced segment (the RS -> AG hand-off) and one "done reading" flag per
