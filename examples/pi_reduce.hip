@@ -70,7 +70,7 @@ int main()
     }
     const bool ok = total == want && std::fabs(4.0 * (double) total / (double) (npoints * (size_t) npes) - M_PI) < 0.05;
     std::cout << "PE#" << my_pe << (ok ? " SUCCESS" : " FAILURE") << " inside " << total << " expected " << want
-              << std::endl;
+              << " npes " << npes << std::endl;
 
     ishmem_free(inside);
     ishmem_finalize();

@@ -18,6 +18,8 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -45,9 +47,28 @@ typedef struct {           /* src/ishmem.h:63-65 */
 #define ISHMEM_TEAM_SHARED  ISHMEMI_C_TEAM_SHARED
 
 /* ---- setup (src/ishmem.h:40-58) ---------------------------------------------------------- */
-inline void ishmem_init(void) { (void) ishmemi_c_init(); }
+/* A failed initialisation is fatal, as in the reference: ishmem_init raises the error and exits
+ * (src/ishmem.cpp:396-407, RAISE_ERROR_MSG src/ishmem/err.h:105-110), a second ishmem_init too. */
+inline void ishmemi_cxx_init_or_exit(void)
+{
+    if (ishmemi_c_initialized()) {
+        fprintf(stderr, "[ishmem_amd] ERROR: Attempt to re-initialize library\n");
+        exit(1);
+    }
+    if (ishmemi_c_init() != 0) {
+        fprintf(stderr, "[ishmem_amd] ERROR: ishmem_init failed: %s\n", ishmemi_c_last_error());
+        exit(1);
+    }
+}
+inline void ishmem_init(void) { ishmemi_cxx_init_or_exit(); }
 inline void ishmem_finalize(void) { (void) ishmemi_c_finalize(); }
-inline int ishmem_init_thread(int requested, int *provided) { return ishmemi_c_init_thread(requested, provided); }
+inline int ishmem_init_thread(int requested, int *provided)
+{
+    (void) requested; /* ISHMEM_THREAD_MULTIPLE is always provided (src/ishmem.cpp:409-419) */
+    ishmemi_cxx_init_or_exit();
+    if (provided) *provided = ISHMEM_THREAD_MULTIPLE;
+    return 0;
+}
 inline void ishmem_query_thread(int *provided) { (void) ishmemi_c_query_thread(provided); }
 inline void ishmem_info_get_version(int *major, int *minor)
 {

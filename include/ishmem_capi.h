@@ -74,15 +74,25 @@ typedef enum {
 
 /* ---- lifecycle — replaces ishmem_init / ishmem_finalize (src/ishmem.h:40-41,
  *      src/ishmem.cpp:224-407) and ishmemx_init_attr (src/ishmemx.h:21-37) ---------------------
- * ishmemi_c_init(): PE identity from the environment: ISHMEM_PE / ISHMEM_NPES, else the
- *   torchrun variables RANK / WORLD_SIZE; device from ISHMEM_DEVICE, else LOCAL_RANK, else 0;
- *   bootstrap key from ISHMEM_BOOTSTRAP_KEY, else derived from MASTER_PORT.
+ * ishmemi_c_init(): PE identity from the process's launcher, where the reference takes it from
+ *   its MPI / PMI runtime (src/runtime/runtime_mpi.cpp:1256-1282), first match wins:
+ *   ISHMEM_PE / ISHMEM_NPES / ISHMEM_DEVICE; torchrun's RANK / WORLD_SIZE / LOCAL_RANK; MPICH
+ *   hydra and Intel MPI (`mpiexec -n N ./app`, test/cmake/common.cmake:28-43) PMI_RANK /
+ *   PMI_SIZE / MPI_LOCALRANKID; Open MPI OMPI_COMM_WORLD_RANK / _SIZE / _LOCAL_RANK; srun
+ *   SLURM_PROCID / SLURM_NTASKS / SLURM_LOCALID.  Device = node-local rank.  Bootstrap key from
+ *   ISHMEM_BOOTSTRAP_KEY, else from the launcher (torchrun's MASTER_PORT, the MPI launcher's
+ *   per-node daemon, the Slurm job step).  A job spread over several nodes is refused.
  * ishmemi_c_init_pe(): the same with explicit values (device < 0: keep the env rule).
+ * ishmemi_c_launch_info(): what ishmemi_c_init would use (no GPU touched): pe, npes, device,
+ *   the launcher's name ("ishmem", "torchrun", "pmi", "openmpi", "slurm", "none") and the
+ *   bootstrap key; nonzero (and ishmemi_c_last_error) when init would refuse it.
  * The bootstrap (handle exchange + host barrier) is a POSIX shared-memory segment on the node;
  * it replaces the reference's MPI/OpenSHMEM/PMI runtime (src/runtime.h:22-84) for the only job
  * it does on this path: exchanging the heap IPC handles (src/ipc.cpp:123-233). */
 int ishmemi_c_init(void);
 int ishmemi_c_init_pe(int pe, int npes, int device, const char *bootstrap_key);
+int ishmemi_c_launch_info(int *pe, int *npes, int *device, char *launcher, size_t launcher_len, char *key,
+                          size_t key_len);
 int ishmemi_c_finalize(void);
 int ishmemi_c_initialized(void);
 int ishmemi_c_my_pe(void);  /* ishmem_my_pe, src/ishmem.h:54 */

@@ -61,9 +61,22 @@ def version() -> str:
 
 # ---- lifecycle ---------------------------------------------------------------------------
 def ishmem_init() -> None:
-    """ishmem_init (src/ishmem.h:40): PE identity from ISHMEM_PE/ISHMEM_NPES or RANK/WORLD_SIZE."""
+    """ishmem_init (src/ishmem.h:40): PE identity from the launcher (ISHMEM_PE / ISHMEM_NPES,
+    torchrun, MPICH hydra / Intel MPI PMI_*, Open MPI OMPI_COMM_WORLD_*, srun SLURM_*; see
+    launch_info)."""
     if _L.ishmemi_c_init() != 0:
         raise RuntimeError(f"ishmem_init failed: {last_error()}")
+
+
+def launch_info() -> dict:
+    """What ishmem_init would use, without touching the GPU: pe, npes, device, launcher, key."""
+    pe, npes, dev = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    launcher, key = ctypes.create_string_buffer(32), ctypes.create_string_buffer(256)
+    rc = _L.ishmemi_c_launch_info(ctypes.byref(pe), ctypes.byref(npes), ctypes.byref(dev), launcher, 32, key, 256)
+    if rc != 0:
+        raise RuntimeError(f"ishmem launch identity refused: {last_error()}")
+    return {"pe": pe.value, "npes": npes.value, "device": dev.value, "launcher": launcher.value.decode(),
+            "key": key.value.decode()}
 
 
 def init(pe: int = 0, npes: int = 1, device: int = -1, key: str | None = None) -> None:

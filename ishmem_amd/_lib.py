@@ -19,6 +19,8 @@ _vp, _i, _sz, _ll, _u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes
 PROTOTYPES = [
     ("ishmemi_c_init", _i, []),
     ("ishmemi_c_init_pe", _i, [_i, _i, _i, ctypes.c_char_p]),
+    ("ishmemi_c_launch_info", _i, [ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.c_char_p, _sz,
+                                   ctypes.c_char_p, _sz]),
     ("ishmemi_c_finalize", _i, []),
     ("ishmemi_c_initialized", _i, []),
     ("ishmemi_c_my_pe", _i, []),

@@ -1420,25 +1420,157 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     return 0;
 }
 
-std::string default_key()
+const char *env_str(const char *name)
 {
-    if (const char *k = getenv("ISHMEM_BOOTSTRAP_KEY")) return k;
-    std::string key = "job";
-    const char *port = getenv("MASTER_PORT"), *run = getenv("TORCHELASTIC_RUN_ID");
-    if (port) key += std::string("_p") + port;
-    if (run) key += std::string("_") + run;
-    // No launcher variables: the PEs of one job are siblings (started by one launcher process),
-    // so its pid keeps concurrent jobs on a node apart.
-    if (!port && !run) key += "_pp" + std::to_string((long) getppid());
-    return key;
+    const char *s = getenv(name);
+    return s && *s ? s : nullptr;
 }
 
-int env_int(const char *a, const char *b, int dflt)
+// Parent pid of process `pid` (/proc/<pid>/stat field 4), or -1.
+long parent_of(long pid)
 {
-    if (const char *s = getenv(a)) return atoi(s);
-    if (b)
-        if (const char *s = getenv(b)) return atoi(s);
-    return dflt;
+    char path[64];
+    snprintf(path, sizeof(path), "/proc/%ld/stat", pid);
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    char buf[512];
+    const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[n] = '\0';
+    const char *rp = strrchr(buf, ')');  // the command name may hold spaces and parentheses
+    long ppid = -1;
+    char state;
+    if (!rp || sscanf(rp + 1, " %c %ld", &state, &ppid) != 2) return -1;
+    return ppid;
+}
+
+// Whether process `pid`'s environment defines `var`; -1 if it cannot be read.
+int env_of_has(long pid, const char *var)
+{
+    char path[64];
+    snprintf(path, sizeof(path), "/proc/%ld/environ", pid);
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    const size_t vl = strlen(var);
+    std::string entry;
+    int found = 0;
+    for (int c; (c = fgetc(f)) != EOF;) {
+        if (c != '\0') {
+            entry.push_back((char) c);
+            continue;
+        }
+        if (entry.size() > vl && entry.compare(0, vl, var) == 0 && entry[vl] == '=') found = 1;
+        entry.clear();
+        if (found) break;
+    }
+    fclose(f);
+    return found;
+}
+
+// The launcher's per-node daemon that started every local rank (hydra_pmi_proxy, orted / prted,
+// slurmstepd): the nearest ancestor whose environment lacks the launcher's rank variable.  Ranks
+// started through a wrapper script (the reference's `mpirun -n N scripts/ishmrun ./app`,
+// test/cmake/common.cmake:28-43) still find the same daemon, hence the same bootstrap key.
+long launcher_daemon(const char *rank_var)
+{
+    long p = (long) getppid();
+    for (int depth = 0; depth < 64 && p > 1; ++depth) {
+        const int has = env_of_has(p, rank_var);
+        if (has == 0) return p;
+        const long pp = parent_of(p);
+        if (has < 0 || pp <= 1) break;
+        p = pp;
+    }
+    return (long) getppid();
+}
+
+// PE identity from the process's launcher.  The reference's ishmem_init takes rank and size from
+// its runtime (MPI: src/runtime/runtime_mpi.cpp:1256-1282; PMI / OpenSHMEM alike); this library
+// has no runtime of its own, so it reads what the launcher exports, first match wins:
+//   ISHMEM_PE / ISHMEM_NPES / ISHMEM_DEVICE   explicit (tests, custom launchers)
+//   RANK / WORLD_SIZE / LOCAL_RANK            torchrun
+//   PMI_RANK / PMI_SIZE / MPI_LOCALRANKID     MPICH hydra, Intel MPI (mpiexec / mpirun)
+//   OMPI_COMM_WORLD_RANK / _SIZE / _LOCAL_RANK  Open MPI
+//   SLURM_PROCID / SLURM_NTASKS / SLURM_LOCALID srun
+// ISHMEM_PE, ISHMEM_NPES, ISHMEM_DEVICE and ISHMEM_BOOTSTRAP_KEY each override the launcher's
+// value.  The device is the node-local rank (one PE per GPU; modulo the visible devices).
+struct LaunchInfo {
+    int pe = 0, npes = 1, local = 0, local_n = 0;
+    std::string launcher = "none", key;
+};
+
+LaunchInfo launch_info()
+{
+    LaunchInfo li;
+    auto num = [](const char *v, int dflt) { return v ? atoi(v) : dflt; };
+    if (env_str("ISHMEM_PE")) {
+        li.launcher = "ishmem";
+        li.pe = num(env_str("ISHMEM_PE"), 0);
+        li.npes = num(env_str("ISHMEM_NPES"), num(env_str("WORLD_SIZE"), 1));
+        li.local = num(env_str("LOCAL_RANK"), 0);
+    } else if (env_str("RANK")) {
+        li.launcher = "torchrun";
+        li.pe = num(env_str("RANK"), 0);
+        li.npes = num(env_str("WORLD_SIZE"), 1);
+        li.local = num(env_str("LOCAL_RANK"), 0);
+        li.local_n = num(env_str("LOCAL_WORLD_SIZE"), 0);
+    } else if (env_str("PMI_RANK")) {
+        li.launcher = "pmi";
+        li.pe = num(env_str("PMI_RANK"), 0);
+        li.npes = num(env_str("PMI_SIZE"), 1);
+        li.local = num(env_str("MPI_LOCALRANKID"), li.pe);
+        li.local_n = num(env_str("MPI_LOCALNRANKS"), 0);
+        li.key = "pmi_d" + std::to_string(launcher_daemon("PMI_RANK"));
+    } else if (env_str("OMPI_COMM_WORLD_RANK")) {
+        li.launcher = "openmpi";
+        li.pe = num(env_str("OMPI_COMM_WORLD_RANK"), 0);
+        li.npes = num(env_str("OMPI_COMM_WORLD_SIZE"), 1);
+        li.local = num(env_str("OMPI_COMM_WORLD_LOCAL_RANK"), li.pe);
+        li.local_n = num(env_str("OMPI_COMM_WORLD_LOCAL_SIZE"), 0);
+        const char *job = env_str("OMPI_MCA_ess_base_jobid") ? env_str("OMPI_MCA_ess_base_jobid") : env_str("PMIX_NAMESPACE");
+        li.key = job ? std::string("ompi_") + job : "ompi_d" + std::to_string(launcher_daemon("OMPI_COMM_WORLD_RANK"));
+    } else if (env_str("SLURM_PROCID") && (env_str("SLURM_NTASKS") || env_str("SLURM_NPROCS"))) {
+        li.launcher = "slurm";
+        li.pe = num(env_str("SLURM_PROCID"), 0);
+        li.npes = num(env_str("SLURM_NTASKS") ? env_str("SLURM_NTASKS") : env_str("SLURM_NPROCS"), 1);
+        li.local = num(env_str("SLURM_LOCALID"), li.pe);
+        li.local_n = num(env_str("SLURM_NTASKS_PER_NODE"), 0);
+        li.key = std::string("slurm_") + (env_str("SLURM_JOB_ID") ? env_str("SLURM_JOB_ID") : "0") + "_" +
+                 (env_str("SLURM_STEP_ID") ? env_str("SLURM_STEP_ID") : "0");
+    }
+    if (env_str("ISHMEM_NPES")) li.npes = num(env_str("ISHMEM_NPES"), li.npes);
+    if (env_str("ISHMEM_DEVICE")) li.local = num(env_str("ISHMEM_DEVICE"), li.local);
+    if (const char *k = env_str("ISHMEM_BOOTSTRAP_KEY")) {
+        li.key = k;
+    } else if (li.key.empty()) {
+        std::string key = "job";
+        const char *port = env_str("MASTER_PORT"), *run = env_str("TORCHELASTIC_RUN_ID");
+        if (port) key += std::string("_p") + port;
+        if (run) key += std::string("_") + run;
+        // No launcher variables: the PEs of one job are siblings (started by one launcher
+        // process), so its pid keeps concurrent jobs on a node apart.
+        if (!port && !run) key += "_pp" + std::to_string((long) getppid());
+        li.key = key;
+    }
+    return li;
+}
+
+std::string default_key() { return launch_info().key; }
+
+// The launcher's identity, checked: this library spans one node (every PE maps every peer's heap),
+// so a job the launcher spread over several nodes is refused instead of becoming several
+// independent worlds.
+int resolve_launch(LaunchInfo &li)
+{
+    li = launch_info();
+    if (li.npes < 1 || li.pe < 0 || li.pe >= li.npes)
+        return fail("init: launcher '" + li.launcher + "' gives PE " + std::to_string(li.pe) + " of " +
+                    std::to_string(li.npes));
+    if (li.local_n > 0 && li.local_n < li.npes && !env_str("ISHMEM_NPES"))
+        return fail("init: the launcher ('" + li.launcher + "') started " + std::to_string(li.npes) +
+                    " PEs but only " + std::to_string(li.local_n) +
+                    " on this node; ishmem_amd's PEs must share one node (xGMI peer mappings)");
+    return 0;
 }
 
 }  // namespace
@@ -1450,16 +1582,28 @@ extern "C" {
 
 int ishmemi_c_init(void)
 {
-    const int pe = env_int("ISHMEM_PE", "RANK", 0);
-    const int npes = env_int("ISHMEM_NPES", "WORLD_SIZE", 1);
-    const int dev = env_int("ISHMEM_DEVICE", "LOCAL_RANK", 0);
-    return init_impl(pe, npes, dev, default_key());
+    LaunchInfo li;
+    if (resolve_launch(li)) return 1;
+    return init_impl(li.pe, li.npes, li.local, li.key);
 }
 
 int ishmemi_c_init_pe(int pe, int npes, int device, const char *key)
 {
-    if (device < 0) device = env_int("ISHMEM_DEVICE", "LOCAL_RANK", 0);
+    if (device < 0) device = launch_info().local;
     return init_impl(pe, npes, device, key && *key ? std::string(key) : default_key());
+}
+
+int ishmemi_c_launch_info(int *pe, int *npes, int *device, char *launcher, size_t launcher_len, char *key,
+                          size_t key_len)
+{
+    LaunchInfo li;
+    const int rc = resolve_launch(li);
+    if (pe) *pe = li.pe;
+    if (npes) *npes = li.npes;
+    if (device) *device = li.local;
+    if (launcher && launcher_len) snprintf(launcher, launcher_len, "%s", li.launcher.c_str());
+    if (key && key_len) snprintf(key, key_len, "%s", li.key.c_str());
+    return rc;
 }
 
 int ishmemi_c_finalize(void)

@@ -5,6 +5,7 @@ grp), ishmem_barrier_all(), ishmem_int_broadcast(...)); only the SYCL launch / q
 Built on the CPU (here and by __graft_entry__.build()); run and result-checked on the GPU, PEs as
 processes sharing the box's GPU."""
 import os
+import shutil
 import subprocess
 import uuid
 from pathlib import Path
@@ -14,6 +15,9 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 EXAMPLES = ["pi_reduce", "library_apis", "team_split_strided"]  # ref: examples/5_, 3_, 6_*.cpp
 HEADERS = [ROOT / "include" / h for h in ("ishmem.h", "ishmemx.h", "ishmem_capi.h", "ishmemx_device.h")]
+MPIEXEC = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
+TORCHRUN_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT", "MASTER_ADDR",
+                 "TORCHELASTIC_RUN_ID")
 
 
 def build_example(name: str) -> Path:
@@ -62,6 +66,28 @@ def test_example_builds(name):
 def test_pi_reduce(npes):
     outs = run_example(build_example("pi_reduce"), npes)
     assert "Value of pi from this experiment" in outs[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not Path(MPIEXEC).exists(), reason="no mpiexec (MPICH hydra)")
+@pytest.mark.parametrize("wrapped", [False, True], ids=["direct", "via_wrapper_script"])
+def test_pi_reduce_under_mpiexec(wrapped):
+    """The reference's launch path (`mpirun -n N scripts/ishmrun ./app`, test/cmake/common.cmake:28-43):
+    `mpiexec -n 2 ./pi_reduce` with no ISHMEM_* or torchrun variable.  The launcher starts both
+    processes before any GPU call; ishmem_init takes PE identity from PMI_RANK / PMI_SIZE /
+    MPI_LOCALRANKID (runtime_mpi.cpp:1256-1282's role) and both PEs must see npes == 2 — before
+    this, each rank became a one-PE world that "reduced" by copying and still printed SUCCESS."""
+    exe = build_example("pi_reduce")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ISHMEM_") and k not in TORCHRUN_VARS}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    cmd = [str(exe)] if not wrapped else ["sh", "-c", '"$0"; exit $?', str(exe)]
+    out = subprocess.run([MPIEXEC, "-n", "2", *cmd], env=env, capture_output=True, text=True, timeout=240)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-3000:]
+    for pe in range(2):
+        assert f"PE#{pe} SUCCESS" in text, text[-3000:]
+    assert text.count(" npes 2") == 2, text[-3000:]
+    assert "Value of pi from this experiment" in text
 
 
 @pytest.mark.gpu

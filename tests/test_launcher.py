@@ -1,0 +1,131 @@
+"""PE identity under the launchers the reference's programs are started with (CPU, no GPU).
+
+The reference's ishmem_init takes rank and size from its MPI / PMI runtime
+(src/runtime/runtime_mpi.cpp:1256-1282); its tests and examples run as
+`mpirun -n N scripts/ishmrun ./app` (test/cmake/common.cmake:28-43).  ishmemi_c_init reads the
+same identity from the launcher's environment (ishmem_amd/csrc/runtime.cpp launch_info) and the
+C++ header's ishmem_init exits on failure like the reference's (src/ishmem.cpp:396-407,
+src/ishmem/err.h:105-110).  The GPU side (the reference's pi example under mpiexec) is
+tests/test_examples.py::test_pi_reduce_under_mpiexec.
+"""
+import ctypes
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+from ishmem_amd import _lib
+
+ROOT = Path(__file__).resolve().parents[1]
+INCLUDE = ROOT / "include"
+MPIEXEC = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
+LAUNCH_VARS = ("ISHMEM_PE", "ISHMEM_NPES", "ISHMEM_DEVICE", "ISHMEM_BOOTSTRAP_KEY", "RANK", "WORLD_SIZE",
+               "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "PMI_RANK", "PMI_SIZE",
+               "MPI_LOCALRANKID", "MPI_LOCALNRANKS", "OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE",
+               "OMPI_COMM_WORLD_LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_SIZE", "SLURM_PROCID", "SLURM_NTASKS",
+               "SLURM_NPROCS", "SLURM_LOCALID", "SLURM_JOB_ID", "SLURM_STEP_ID", "SLURM_NTASKS_PER_NODE")
+
+# One process: what ishmemi_c_init would use, then (optionally) the native bootstrap's allgather
+# among the PEs it names.
+PROBE = r'''
+import ctypes, sys
+sys.path.insert(0, sys.argv[1])
+from ishmem_amd import _lib
+L = _lib.load(build_if_missing=False)
+pe, npes, dev = ctypes.c_int(-9), ctypes.c_int(-9), ctypes.c_int(-9)
+launcher, key = ctypes.create_string_buffer(32), ctypes.create_string_buffer(256)
+rc = L.ishmemi_c_launch_info(ctypes.byref(pe), ctypes.byref(npes), ctypes.byref(dev), launcher, 32, key, 256)
+line = f"rc={rc} pe={pe.value} npes={npes.value} dev={dev.value} launcher={launcher.value.decode()}"
+if rc:
+    line += " err=" + L.ishmemi_c_last_error().decode().replace(" ", "_")
+elif len(sys.argv) > 2 and npes.value > 1:
+    out = (ctypes.c_int * npes.value)()
+    r = L.ishmemi_c_bootstrap_selftest(pe.value, npes.value, key.value, 10 * pe.value + 1, out)
+    line += f" boot={r} got={','.join(str(v) for v in out)}"
+print(line, flush=True)
+'''
+
+
+def clean_env(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in LAUNCH_VARS}
+    env.update({k: str(v) for k, v in extra.items()})
+    return env
+
+
+def probe(env, boot=False):
+    args = [sys.executable, "-c", PROBE, str(ROOT)] + (["boot"] if boot else [])
+    out = subprocess.run(args, env=env, capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    return dict(kv.split("=", 1) for kv in out.stdout.split())
+
+
+def test_launch_info_reads_each_launcher_family():
+    assert probe(clean_env()) == {"rc": "0", "pe": "0", "npes": "1", "dev": "0", "launcher": "none"}
+    got = probe(clean_env(ISHMEM_PE=2, ISHMEM_NPES=4, ISHMEM_DEVICE=1))
+    assert (got["pe"], got["npes"], got["dev"], got["launcher"]) == ("2", "4", "1", "ishmem")
+    got = probe(clean_env(RANK=1, WORLD_SIZE=8, LOCAL_RANK=5, MASTER_PORT=29500))
+    assert (got["pe"], got["npes"], got["dev"], got["launcher"]) == ("1", "8", "5", "torchrun")
+    got = probe(clean_env(PMI_RANK=3, PMI_SIZE=8, MPI_LOCALRANKID=3, MPI_LOCALNRANKS=8))
+    assert (got["pe"], got["npes"], got["dev"], got["launcher"]) == ("3", "8", "3", "pmi")
+    got = probe(clean_env(OMPI_COMM_WORLD_RANK=6, OMPI_COMM_WORLD_SIZE=8, OMPI_COMM_WORLD_LOCAL_RANK=6,
+                          OMPI_COMM_WORLD_LOCAL_SIZE=8))
+    assert (got["pe"], got["npes"], got["dev"], got["launcher"]) == ("6", "8", "6", "openmpi")
+    got = probe(clean_env(SLURM_PROCID=7, SLURM_NTASKS=8, SLURM_LOCALID=7, SLURM_JOB_ID=42))
+    assert (got["pe"], got["npes"], got["dev"], got["launcher"]) == ("7", "8", "7", "slurm")
+    # Explicit variables override the launcher's, one by one.
+    got = probe(clean_env(PMI_RANK=1, PMI_SIZE=2, MPI_LOCALRANKID=1, ISHMEM_DEVICE=0))
+    assert (got["pe"], got["npes"], got["dev"], got["launcher"]) == ("1", "2", "0", "pmi")
+
+
+def test_launch_info_refuses_multi_node_and_bad_ranks():
+    got = probe(clean_env(PMI_RANK=0, PMI_SIZE=4, MPI_LOCALRANKID=0, MPI_LOCALNRANKS=2))
+    assert got["rc"] == "1" and "one_node" in got["err"], got
+    got = probe(clean_env(ISHMEM_PE=3, ISHMEM_NPES=2))
+    assert got["rc"] == "1", got
+
+
+@pytest.mark.skipif(not Path(MPIEXEC).exists(), reason="no mpiexec (MPICH hydra)")
+@pytest.mark.parametrize("wrapped", [False, True], ids=["direct", "via_wrapper_script"])
+def test_mpiexec_two_ranks_form_one_world(wrapped):
+    """`mpiexec -n 2` with no ISHMEM_* / torchrun variables: both ranks resolve PE 0 / 1 of 2 and
+    meet in the native bootstrap (allgather + barrier).  Wrapped: each rank runs under its own shell,
+    like the reference's `mpirun -n N scripts/ishmrun ./app`, and the key still agrees (the hydra
+    proxy, found by walking up the process tree)."""
+    cmd = [sys.executable, "-c", PROBE, str(ROOT), "boot"]
+    if wrapped:  # sh stays the rank's process (no exec), python its child
+        cmd = ["sh", "-c", f'"{sys.executable}" -c "$0" "$@"; exit $?', PROBE, str(ROOT), "boot"]
+    out = subprocess.run([MPIEXEC, "-n", "2", *cmd], env=clean_env(), capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = sorted(l for l in out.stdout.splitlines() if l.startswith("rc="))
+    assert len(lines) == 2, out.stdout + out.stderr
+    got = [dict(kv.split("=", 1) for kv in l.split()) for l in lines]
+    assert [g["pe"] for g in got] == ["0", "1"]
+    for g in got:
+        assert (g["rc"], g["npes"], g["launcher"], g["boot"], g["got"]) == ("0", "2", "pmi", "0", "1,11"), g
+
+
+def test_cxx_ishmem_init_failure_exits_like_the_reference(tmp_path):
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    src = tmp_path / "t.cpp"
+    src.write_text('#include <ishmem.h>\n#include <cstdio>\n'
+                   'int main() { ishmem_init(); std::printf("after init\\n"); return 0; }\n')
+    exe = tmp_path / "t"
+    subprocess.run([gxx, "-std=c++17", f"-I{INCLUDE}", str(src), "-o", str(exe),
+                    f"-L{_lib.LIB_PATH.parent}", f"-Wl,-rpath,{_lib.LIB_PATH.parent}", "-lishmem_amd"], check=True)
+    # PE 3 of 2: refused before any GPU call, on any machine.
+    out = subprocess.run([str(exe)], env=clean_env(ISHMEM_PE=3, ISHMEM_NPES=2), capture_output=True, text=True,
+                         timeout=60)
+    assert out.returncode == 1, (out.returncode, out.stdout, out.stderr)
+    assert "after init" not in out.stdout
+    assert "ishmem_init failed" in out.stderr and "PE 3 of 2" in out.stderr, out.stderr
+
+
+def test_launch_info_is_declared_and_bound():
+    L = _lib.load()
+    assert L.ishmemi_c_launch_info.restype is ctypes.c_int
