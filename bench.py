@@ -286,8 +286,9 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     """N>1: the f32 sum again under other launch shapes, set alike on every rank, so the driver's
     multi-GPU run records how the xGMI path responds (data for choosing the defaults; one
     MI355X per PE cannot be rehearsed on a one-GPU box):
-      grid  - the payload with the workgroup cap at 128 / 256 / 512 / 1024 (then clamped to the
-              resident capacity);
+      wait  - the persistent kernel (phased path off) at 1 / 4 / 16 MiB with wait_slots 4 / 8 / 16 /
+              32: each waiting launch may hold 1 / wait_slots of the device (kernels.h, "Waiting
+              footprint"; 16 = 64 workgroups is the default) — whether that grid fills the links;
       phased - 4 / 16 / 64 MiB and the payload on the phased path (one-shot grids between
                barriers) and on the persistent kernel (the phased threshold);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
@@ -312,21 +313,23 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
 
     out = []
 
-    def run(case, param, value, nbytes, iters):
-        old = ish.get_param(param)
-        ish.set_param(param, value)
+    def run(case, param, value, nbytes, iters, also=None):
+        params = {param: value, **(also or {})}
+        old = {k: ish.get_param(k) for k in params}
+        for k, v in params.items():
+            ish.set_param(k, v)
         try:
             ms = timed(nbytes // 4, iters)
         finally:
-            ish.set_param(param, old)
-        out.append({"case": case, param: value, "bytes": nbytes, "us": round(ms * 1e3, 2),
+            for k, v in old.items():
+                ish.set_param(k, v)
+        out.append({"case": case, **params, "bytes": nbytes, "us": round(ms * 1e3, 2),
                     "algbw_GiBps": round(nbytes / GiB / (ms * 1e-3), 2)})
 
-    # Several PEs sharing one GPU (ISHMEM_BENCH_SAME_DEVICE rehearsals) keep the cap they started with.
-    cap = ish.get_param("max_blocks") if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else 1024
-    for mb in (128, 256, 512, 1024):
-        if mb <= cap:
-            run("grid", "max_blocks", mb, B, 5)
+    for ws in (4, 8, 16, 32):
+        for nb in (1 << 20, 4 << 20, 16 << 20):
+            if nb <= B:
+                run("wait", "wait_slots", ws, nb, 20, also={"phased_min_bytes": -1})
     for nb in sorted({4 << 20, 16 << 20, 64 << 20, B}):
         if nb <= B:
             run("phased", "phased_min_bytes", 0, nb, 5 if nb == B else 20)

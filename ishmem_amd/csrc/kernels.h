@@ -190,6 +190,19 @@ hipError_t launch_pull_probe(const FaninArgs &a, int policy, hipStream_t s);
 // co-located peer needs to make progress (across GPUs that cannot happen).
 void set_device_share(int share);
 int device_share();
+// Waiting footprint (round 4).  The kernels whose workgroups wait for peers — the persistent
+// reduce (start handshake, segment hand-offs), the small-message rings, the persistent collect /
+// scan — each take at most 1 / (share x wait_slots) of the device's resident workgroups.  A
+// device can then hold wait_slots such launches of every co-located PE at once, so a launch whose
+// workgroups wait for a peer can never keep a kernel of another team (on another stream, issued in
+// the other order on that peer) from becoming resident: collectives of different teams may be in
+// flight together, as in the reference (src/teams.h:29-38).  With one PE per GPU and HIP's 4
+// hardware queues per process (GPU_MAX_HW_QUEUES) at most 4 kernels of a process run at once, so
+// the default 16 keeps a 4x margin (ISHMEM_WAIT_SLOTS).  The phased grids and the fan-in kernel
+// never wait and keep the whole device.
+constexpr int kWaitSlotsDefault = 16;
+void set_wait_slots(int slots);
+int wait_slots();
 // Test hook: `grid` workgroups that each hold half a CU (1024 work-items, 80 KiB LDS) for `usec`.
 hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s);
 hipError_t launch_produce_u32(uint32_t *dst, const uint32_t *a, const uint32_t *b, uint64_t n, hipStream_t s);

@@ -6,9 +6,12 @@ namespace ishmemi {
 
 namespace {
 int g_device_share = 1;
+int g_wait_slots = kWaitSlotsDefault;
 }
 void set_device_share(int share) { g_device_share = share < 1 ? 1 : share; }
 int device_share() { return g_device_share; }
+void set_wait_slots(int slots) { g_wait_slots = slots < 1 ? 1 : slots; }
+int wait_slots() { return g_wait_slots; }
 
 #define ISHMEMI_DECL_OP(N)                                                                         \
     hipError_t launch_allreduce_op##N(int dt, bool vec, const ReduceArgs &a, int grid,             \

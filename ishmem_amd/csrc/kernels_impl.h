@@ -1129,27 +1129,32 @@ __device__ __forceinline__ uint64_t fold8(uint64_t acc, uint64_t x)
     return __builtin_bit_cast(uint64_t, a);
 }
 
+// The grid is capped by the waiting footprint (resident_blocks_of), so a thread may own several
+// items (t, t + G*kBlock, ...): it pushes all of them before polling for any.
+template <typename T>
+__device__ __forceinline__ uint64_t ll_load(const LLArgs &a, uint64_t off, uint64_t valid)
+{
+    if (valid == 8) return *(const uint64_t *) (a.src + off);
+    // Ragged last item: byte assembly (a variable-length memcpy would go through scratch).
+    uint64_t mine = 0;
+    for (uint32_t k = 0; k < (uint32_t) valid; ++k) mine |= (uint64_t) (uint8_t) a.src[off + k] << (8 * k);
+    return mine;
+}
+
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
 {
-    const uint64_t item = (uint64_t) blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t first = (uint64_t) blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t stride = (uint64_t) gridDim.x * kBlock;
     const uint64_t nitems = (a.nbytes + 7) / 8;
     const int p = a.p, me = a.me;
     const uint32_t ep = kernel_epoch(a);
     const uint64_t par = ep & 1u;
     const uint64_t tag = (uint64_t) ep << 32;
     bool ok = true;
-    if (item < nitems) {
+    for (uint64_t item = first; item < nitems; item += stride) {
         const uint64_t off = item * 8;
-        const uint64_t valid = a.nbytes - off < 8 ? a.nbytes - off : 8;
-        uint64_t mine = 0;
-        if (valid == 8) {
-            mine = *(const uint64_t *) (a.src + off);
-        } else {
-            // Ragged last item: byte assembly (a variable-length memcpy would go through scratch).
-            for (uint32_t k = 0; k < (uint32_t) valid; ++k)
-                mine |= (uint64_t) (uint8_t) a.src[off + k] << (8 * k);
-        }
+        const uint64_t mine = ll_load<T>(a, off, a.nbytes - off < 8 ? a.nbytes - off : 8);
         const uint64_t g0 = tag | (uint32_t) mine, g1 = tag | (uint32_t) (mine >> 32);
         for (int j = 0; j < p; ++j) {
             if (j == me) continue;
@@ -1157,8 +1162,13 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
             __hip_atomic_store(slot, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(slot + 1, g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint64_t item = first; item < nitems && ok; item += stride) {
+        const uint64_t off = item * 8;
+        const uint64_t valid = a.nbytes - off < 8 ? a.nbytes - off : 8;
+        const uint64_t mine = ll_load<T>(a, off, valid);
         uint64_t acc = 0;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (int j = 0; j < p && ok; ++j) {
             uint64_t x = mine;
             if (j != me) {
@@ -1192,12 +1202,15 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
     kernel_epoch_done(a, ep);
 }
 
+inline int resident_blocks_of(const void *kernel);
+
 template <typename T, int OP>
 hipError_t ll_t(const LLArgs &a, hipStream_t s)
 {
     const uint64_t nitems = (a.nbytes + 7) / 8;
-    const int grid = (int) ((nitems + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL((ll_kernel<T, OP>), dim3(grid > 0 ? grid : 1), dim3(kBlock), 0, s, a);
+    const uint64_t want = std::max<uint64_t>(1, (nitems + kBlock - 1) / kBlock);
+    const int grid = (int) std::min<uint64_t>(want, (uint64_t) resident_blocks_of((const void *) ll_kernel<T, OP>));
+    hipLaunchKernelGGL((ll_kernel<T, OP>), dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
@@ -1216,15 +1229,19 @@ __global__ __launch_bounds__(kBlock) void team_sync_kernel(ReduceArgs a)
 template <int OP, typename S, typename U>
 using Canon = std::conditional_t<(OP == ISHMEMI_OP_MAX || OP == ISHMEMI_OP_MIN), S, U>;
 
-// Workgroups of `kernel` that are resident at once on this device (occupancy API, cached per
-// kernel address), divided among the PEs sharing the device.  The collectives are correct with
-// any residency of their grid (owned work can be stolen, the rest is grabbed; nothing is paired),
-// so the answer need not be exact (the API can over-report by one block per CU for SGPR-heavy
-// kernels, MI355X_MICROARCH.md residency): the clamp only avoids launching workgroups that would
-// queue behind the first wave, and keeps co-located PEs' launches from crowding each other out.
+// Grid cap of a kernel whose workgroups wait for peers (kernels.h, "Waiting footprint"): the
+// workgroups of `kernel` resident at once on this device (occupancy API, cached per kernel
+// address; it can over-report by one block per CU for SGPR-heavy kernels, MI355X_MICROARCH.md
+// residency, which the division leaves far from mattering) divided by share x wait_slots.  The collectives are
+// correct with any residency of their grid (owned work can be stolen, the rest is grabbed or
+// strided; nothing is paired), so the cap only bounds how much of the device one waiting launch
+// can hold.  Round 3 sized the persistent reduce to the whole device (1024 workgroups, each
+// spinning at start): two collectives of different teams issued in opposite orders on two PEs
+// then each held their own GPU while waiting for the other's kernel, which could not get a CU —
+// the r03zh device timeouts (profiles/r03/phased_share/).
 inline int resident_blocks_of(const void *kernel)
 {
-    static std::mutex mu;
+    static std::mutex mu;  // one instance per translation unit (inline, internal namespace)
     static std::map<const void *, int> cache;
     static int cus = 0;
     std::lock_guard<std::mutex> lk(mu);
@@ -1236,24 +1253,20 @@ inline int resident_blocks_of(const void *kernel)
             cus = 1;
         }
     }
+    int per = 0;
     auto it = cache.find(kernel);
     if (it != cache.end()) {
-        const int per = it->second, pe_share = device_share();
-        const int per_cu = pe_share > 1 && per > 1 ? per - 1 : per;
-        return std::max(1, per_cu * std::max(cus, 1) / pe_share);
+        per = it->second;
+    } else {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess) {
+            (void) hipGetLastError();
+            per = 1;
+        }
+        per = std::max(per, 1);
+        cache[kernel] = per;
     }
-    int per = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess) {
-        (void) hipGetLastError();
-        per = 1;
-    }
-    cache[kernel] = std::max(per, 1);
-    // PEs sharing the GPU: one block per CU of margin, so every co-located PE's grid is
-    // resident at once even where the API over-reports — a PE none of whose workgroups is
-    // resident could not even announce its launch while its peers' workgroups wait for it.
-    const int pe_share = device_share();
-    const int per_cu = pe_share > 1 && per > 1 ? per - 1 : std::max(per, 1);
-    return std::max(1, per_cu * std::max(cus, 1) / pe_share);
+    const long long slots = (long long) device_share() * wait_slots();
+    return (int) std::max<long long>(1, (long long) per * std::max(cus, 1) / slots);
 }
 
 template <typename K>

@@ -63,40 +63,67 @@ int hipfail(const char *what, hipError_t e)
         if (e_ != hipSuccess) return hipfail(#expr, e_);                                           \
     } while (0)
 
-size_t parse_size(const char *s, size_t dflt)
+// Byte counts from the environment: plain bytes or with a K / M / G / T suffix (powers of 1024),
+// optionally followed by "iB" or "B" ("16M", "16MiB", "16MB"); surrounding blanks allowed.  Anything
+// else (trailing junk, no digits, NaN) is an error that fails init: these values choose kernel
+// paths every PE must agree on, so a typo must not parse as something else.  Values past
+// LLONG_MAX clamp to it; negative values mean "off" (-1) where the variable allows it.
+std::string g_env_error;  // first malformed variable seen by init's parsing
+
+bool parse_bytes(const char *s, long long &out)
 {
-    if (!s || !*s) return dflt;
+    while (*s == ' ' || *s == '\t') ++s;
     char *end = nullptr;
     double v = strtod(s, &end);
-    if (end && *end) {
-        switch (*end) {
-            case 'k': case 'K': v *= 1024.0; break;
-            case 'm': case 'M': v *= 1024.0 * 1024.0; break;
-            case 'g': case 'G': v *= 1024.0 * 1024.0 * 1024.0; break;
-            default: break;
-        }
+    if (end == s || v != v) return false;
+    double mul = 1.0;
+    switch (*end) {
+        case 'k': case 'K': mul = 1024.0; ++end; break;
+        case 'm': case 'M': mul = 1024.0 * 1024.0; ++end; break;
+        case 'g': case 'G': mul = 1024.0 * 1024.0 * 1024.0; ++end; break;
+        case 't': case 'T': mul = 1024.0 * 1024.0 * 1024.0 * 1024.0; ++end; break;
+        default: break;
     }
-    return v > 0 ? (size_t) v : dflt;
+    if (mul > 1.0 && (*end == 'i' || *end == 'I')) ++end;
+    if (*end == 'b' || *end == 'B') ++end;
+    while (*end == ' ' || *end == '\t') ++end;
+    if (*end) return false;
+    v *= mul;
+    if (v < 0) out = -1;
+    else if (v >= 9.2233720368547748e18) out = std::numeric_limits<long long>::max();
+    else out = (long long) v;
+    return true;
+}
+
+long long env_bytes(const char *name, long long dflt)
+{
+    const char *s = getenv(name);
+    if (!s || !*s) return dflt;
+    long long v = 0;
+    if (!parse_bytes(s, v)) {
+        if (g_env_error.empty())
+            g_env_error = std::string(name) + "='" + s + "' is not a byte count (digits, then K / M / G / T)";
+        return dflt;
+    }
+    return v;
+}
+
+// Sizes that must be positive (heap, staging).
+size_t env_size(const char *name, size_t dflt)
+{
+    const long long v = env_bytes(name, (long long) dflt);
+    if (v <= 0) {
+        if (g_env_error.empty() && getenv(name) && *getenv(name))
+            g_env_error = std::string(name) + " must be a positive byte count";
+        return dflt;
+    }
+    return (size_t) v;
 }
 
 long long env_ll(const char *name, long long dflt)
 {
     const char *s = getenv(name);
     return (s && *s) ? atoll(s) : dflt;
-}
-
-// A byte-count variable: plain bytes or with a K / M / G suffix ("16M"), 0 allowed, negative = -1.
-long long env_bytes(const char *name, long long dflt)
-{
-    const char *s = getenv(name);
-    if (!s || !*s) return dflt;
-    char *end = nullptr;
-    double v = strtod(s, &end);
-    if (end == s) return dflt;
-    if (*end == 'k' || *end == 'K') v *= 1024.0;
-    else if (*end == 'm' || *end == 'M') v *= 1024.0 * 1024.0;
-    else if (*end == 'g' || *end == 'G') v *= 1024.0 * 1024.0 * 1024.0;
-    return v < 0 ? -1 : (long long) v;
 }
 
 struct Team {
@@ -112,10 +139,10 @@ constexpr long long kPhasedOff = std::numeric_limits<long long>::max();
 // fold's 42 / 78 us; 4 PEs x 16 MiB 40 vs 48 us; at 8 MiB and below the extra barrier round trips
 // cost what the one-shot grids save.
 constexpr long long kPhasedDefault = 16ll << 20;
-// ...unless more PEs than this share one GPU (rehearsals only): the phased path's three barriers
-// are separate launches, and when eight processes time-slice one GPU each costs ~40-80 us
-// (8 PEs x 1 GiB: 3.94 vs 3.88 ms; scan 1817 vs 1606 us).  A PE that sets the variable keeps it.
-constexpr int kPhasedMaxShare = 4;
+// Round 3 turned it off when more than 4 PEs shared one GPU (co-located rehearsals, where the
+// three barrier launches cost ~40-80 us each among eight time-sliced processes).  Round 4 drops
+// that rule: co-located runs take the path one PE per GPU takes, so the 8-PE tests at BASELINE's
+// sizes exercise rs_phase_kernel<P=8> + ag_phase_kernel.
 
 struct PeRecord {
     int32_t pe, pid, device, flags_kind;
@@ -125,7 +152,6 @@ struct PeRecord {
     // Launch-shape parameters: the multi-PE kernels pair workgroup b with workgroup b of every
     // peer and choose the LL path per call, so every PE must use the same values.
     int64_t max_blocks, ll_max_bytes, oneshot_p2, phased_min;
-    int32_t phased_explicit;  // ISHMEM_PHASED_MIN_BYTES was set for this PE
     uint64_t staging_bytes;
     int64_t staging_slots;
     hipIpcMemHandle_t heap_handle;
@@ -664,8 +690,13 @@ int reduce_staged(State &s, int team, int op, int dt, void *dst, const void *src
 {
     const size_t bytes = n * dtype_size(dt);
     CallPins pins;
-    pins.pin(const_cast<void *>(src), bytes);
-    pins.pin(dst, bytes);
+    // Not while the stream is being captured into a hipGraph: the synchronize below would
+    // invalidate the capture, and the buffers would be unlocked again before any replay.  The
+    // captured copies then stay HIP's own pageable copies.
+    if (!capturing(st)) {
+        pins.pin(const_cast<void *>(src), bytes);
+        pins.pin(dst, bytes);
+    }
     int rc = reduce_staged_pipeline(s, team, op, dt, dst, src, n, ret, st);
     if (pins.any()) {
         // Every copy of the call has completed (also after a failure part-way) before unlocking.
@@ -1188,6 +1219,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.pe = pe;
     s.npes = npes;
     set_device_share(1);
+    set_wait_slots((int) std::min<long long>(1 << 20, std::max<long long>(1, env_ll("ISHMEM_WAIT_SLOTS", kWaitSlotsDefault))));
     s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, env_ll("ISHMEM_MAX_BLOCKS", kMaxBlocks)));
     s.timeout_ms = std::max<long long>(1, env_ll("ISHMEM_TIMEOUT_MS", 60000));
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
@@ -1198,9 +1230,15 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.oneshot_p2 = std::max<long long>(0, env_bytes("ISHMEM_ONESHOT_P2_MAX_BYTES", 64ll << 20));
     s.phased_min = env_bytes("ISHMEM_PHASED_MIN_BYTES", kPhasedDefault);
     if (s.phased_min < 0) s.phased_min = kPhasedOff;
-    s.staging_bytes = (parse_size(getenv("ISHMEM_STAGING_SIZE"), (size_t) 128 << 20) + kHeapAlign - 1) &
+    s.staging_bytes = (env_size("ISHMEM_STAGING_SIZE", (size_t) 128 << 20) + kHeapAlign - 1) &
                       ~(size_t) (kHeapAlign - 1);
     s.staging_slots = (int) std::min<long long>(kMaxStagingSlots, std::max<long long>(2, env_ll("ISHMEM_STAGING_SLOTS", 4)));
+    const size_t heap_request = env_size("ISHMEM_SYMMETRIC_SIZE", (size_t) 4 << 30);
+    if (!g_env_error.empty()) {
+        const std::string e = g_env_error;
+        g_env_error.clear();
+        return fail("init: " + e);
+    }
 
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
@@ -1209,7 +1247,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     HIP_TRY(hipSetDevice(s.device));
 
     // Symmetric heap: ONE hipMalloc (coarse-grained HBM) per PE, src/memory.cpp:35-132.
-    s.heap_size = parse_size(getenv("ISHMEM_SYMMETRIC_SIZE"), (size_t) 4 << 30);
+    s.heap_size = heap_request;
     s.heap_size = (s.heap_size + (2u << 20) - 1) & ~(size_t) ((2u << 20) - 1);
     HIP_TRY(hipMalloc((void **) &s.heap, s.heap_size));
     s.free_list.clear();
@@ -1255,7 +1293,6 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.ll_max_bytes = s.ll_max_bytes;
         mine.oneshot_p2 = s.oneshot_p2;
         mine.phased_min = s.phased_min;
-        mine.phased_explicit = getenv("ISHMEM_PHASED_MIN_BYTES") && *getenv("ISHMEM_PHASED_MIN_BYTES");
         mine.staging_bytes = s.staging_bytes;
         mine.staging_slots = s.staging_slots;
         if (hipDeviceGetPCIBusId(mine.pci_bus, sizeof(mine.pci_bus), s.device) != hipSuccess) {
@@ -1286,16 +1323,6 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         bool coarse_forced = false;  // a test asked for coarse-grained flags (ISHMEM_FLAGS_KIND=2)
         for (int j = 0; j < npes; ++j) coarse_forced = coarse_forced || all[j].flags_kind_requested == kFlagsCoarse;
         set_device_share(share);
-        // The phased default by topology, from records every PE holds (so every PE decides alike).
-        int max_share = 0;
-        bool phased_explicit = false;
-        for (int j = 0; j < npes; ++j) {
-            int sj = 0;
-            for (int k = 0; k < npes; ++k) sj += strncmp(all[j].pci_bus, all[k].pci_bus, sizeof(mine.pci_bus)) == 0;
-            max_share = std::max(max_share, sj);
-            phased_explicit = phased_explicit || all[j].phased_explicit;
-        }
-        if (!phased_explicit && max_share > kPhasedMaxShare) s.phased_min = kPhasedOff;
         for (int j = 0; j < npes; ++j) {
             if (j == pe) continue;
             if (all[j].heap_size != s.heap_size)
@@ -2318,6 +2345,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     std::lock_guard<std::mutex> lk(s.mu);
     const std::string n = name ? name : "";
     if (n == "max_blocks") s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, value));
+    else if (n == "wait_slots") set_wait_slots((int) std::min<long long>(1 << 20, std::max<long long>(1, value)));
     else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
     else if (n == "stream_order") s.stream_order = value != 0;
     else if (n == "oneshot_p2_max_bytes") s.oneshot_p2 = std::max<long long>(0, value);
@@ -2339,6 +2367,7 @@ long long ishmemi_c_get_param(const char *name)
     State &s = S();
     const std::string n = name ? name : "";
     if (n == "max_blocks") return s.max_blocks;
+    if (n == "wait_slots") return wait_slots();
     if (n == "timeout_ms") return s.timeout_ms;
     if (n == "stream_order") return s.stream_order ? 1 : 0;
     if (n == "oneshot_p2_max_bytes") return s.oneshot_p2;

@@ -4,6 +4,7 @@
 // of its reduce_*.cpp pattern tests (sources = reference source patterns, checked against the
 // reference check patterns restated in oracle/oracle.c, linked here as the CHECKER).
 // Also: a wavefront (sub_group) caller and a single work-item device-side ishmem_int_sum_reduce,
+// the reference's device_multi_wg mode (k work-groups of one kernel, each on its own team clone),
 // and the device-side fcollect / collect / sum_inscan / sum_exscan (closed-form checks).
 // Every device call is the reference's context-free form (the library's device state reaches the
 // kernels through include/ishmemx_device.h's per-code-object context slot); groups are HIP
@@ -85,6 +86,29 @@ __global__ void wave_kernel(float *dest, const float *source, size_t n,
     if (threadIdx.x / warpSize != 1) return;
     const int r = ishmemx_float_sum_reduce_work_group(dest, source, n, ishmemx_dev::wavefront);
     if (__lane_id() == 0) *rc = r;
+}
+
+// device_multi_wg (ishmem_tester.h:117, :299-304, :1256-1260; team_reduce_test.h:119-137): k
+// work-groups of ONE kernel, work-group g reducing its own slice [g * per, (g + 1) * per) on its
+// own clone of TEAM_WORLD (ishmem_team_split_strided(WORLD, 0, 1, npes), ishmem_tester.h:299-304),
+// the division of the tester's bandwidth runs (nelems /= groups, ishmem_tester.h:1292, :1344-1347).
+// k collectives of k different teams in flight inside one kernel; each team has its own device
+// flag rows and epoch counter.
+struct WgTeams {
+    int t[8];
+};
+
+template <typename T, int OPC>
+__global__ void multi_wg_kernel(WgTeams teams, T *dest, const T *source, size_t per, int *rc)
+{
+    const size_t off = (size_t) blockIdx.x * per;
+    const int team = teams.t[blockIdx.x];
+    int r;
+    if constexpr (OPC == ISHMEMI_OP_SUM) r = ishmemx_sum_reduce_work_group(team, dest + off, source + off, per, cg::this_thread_block());
+    else if constexpr (OPC == ISHMEMI_OP_MIN) r = ishmemx_min_reduce_work_group(team, dest + off, source + off, per, cg::this_thread_block());
+    else if constexpr (OPC == ISHMEMI_OP_PROD) r = ishmemx_prod_reduce_work_group(team, dest + off, source + off, per, cg::this_thread_block());
+    else r = ishmemx_xor_reduce_work_group(team, dest + off, source + off, per, cg::this_thread_block());
+    if (threadIdx.x == 0) rc[blockIdx.x] = r;
 }
 
 // Device-side blocking call by one work-item (the reference's single_task shape).
@@ -211,6 +235,39 @@ static void pattern_case(size_t n, dim3 block, char *sb, char *db,
     }
 }
 
+template <typename T, int OPC, int ODT>
+static void multi_wg_case(const WgTeams &teams, int k, size_t n, int block, char *sb, char *db, int *rc)
+{
+    const int pe = ishmem_my_pe(), npes = ishmem_n_pes();
+    const int fam = OPC == OR_XOR ? PAT_XOR : PAT_ARITH;
+    const size_t per = n / (size_t) k, covered = per * (size_t) k;
+    std::vector<T> src(n), chk(n), got(n);
+    oracle_pattern_source(fam, ODT, pe, n, src.data());
+    oracle_pattern_check(fam, OPC, ODT, npes, n, chk.data());
+    (void) hipMemcpy(sb, src.data(), n * sizeof(T), hipMemcpyHostToDevice);
+    (void) hipMemset(db, 0x5A, n * sizeof(T));
+    (void) hipMemset(rc, 0xff, 8 * sizeof(int));
+    ishmem_barrier_all();  // every PE's source is in place (ishmem_sync_all in TEST_MULTI_WG_FN)
+    hipLaunchKernelGGL((multi_wg_kernel<T, OPC>), dim3(k), dim3(block), 0, 0, teams, (T *) db, (const T *) sb, per,
+                       rc);
+    (void) hipDeviceSynchronize();
+    int r[8];
+    (void) hipMemcpy(r, rc, sizeof(r), hipMemcpyDeviceToHost);
+    (void) hipMemcpy(got.data(), db, n * sizeof(T), hipMemcpyDeviceToHost);
+    int rbad = 0;
+    for (int g = 0; g < k; ++g) rbad += r[g] != 0;
+    size_t bad = 0;
+    for (size_t i = 0; i < covered; ++i) bad += memcmp(&got[i], &chk[i], sizeof(T)) != 0;
+    std::vector<T> guard(1);
+    memset(guard.data(), 0x5A, sizeof(T));
+    for (size_t i = covered; i < n; ++i) bad += memcmp(&got[i], guard.data(), sizeof(T)) != 0;  // untouched
+    if (rbad || bad) {
+        if (++errors <= 16)
+            printf("[%d] FAIL device_multi_wg op %d dt %d k %d n %zu block %d rc-fail %d bad %zu\n", pe, OPC, ODT, k,
+                   n, block, rbad, bad);
+    }
+}
+
 // Device-side broadcast (ishmemx_broadcastmem_work_group / ishmem_<TN>_broadcast, the reference's
 // intra-node pull): the source is produced in the kernel, every member pulls the root's bytes.
 __global__ void bcast_kernel(char *dest, char *source, size_t nbytes, int root, int my_pe, int mode, int *rc)
@@ -269,7 +326,7 @@ int main()
     const size_t maxn = 1 << 17;
     char *sb = (char *) ishmem_malloc(maxn * 8);
     char *db = (char *) ishmem_malloc(maxn * 8);
-    int *rc = (int *) ishmem_malloc(sizeof(int));
+    int *rc = (int *) ishmem_malloc(8 * sizeof(int));
 
     for (size_t n = 1; n <= maxn; n <<= 2) {
         for (int block : {64, 256, 1024}) {
@@ -337,6 +394,27 @@ int main()
                                                                     db, rc);
         group_case<decltype(&single_kernel), int, OR_SUM, OD_INT32>("single-thread int sum", single_kernel, 1, n,
                                                                     sb, db, rc);
+    }
+    // device_multi_wg: k = 1..4 work-groups of one kernel on k clones of TEAM_WORLD.
+    {
+        WgTeams teams{};
+        for (int g = 0; g < 4; ++g) {
+            teams.t[g] = ISHMEM_TEAM_INVALID;
+            if (ishmem_team_split_strided(ISHMEM_TEAM_WORLD, 0, 1, npes, nullptr, 0, &teams.t[g]) != 0 ||
+                teams.t[g] == ISHMEM_TEAM_INVALID) {
+                if (++errors <= 16) printf("[%d] FAIL team clone %d: %s\n", pe, g, ishmemi_c_last_error());
+            }
+        }
+        for (int k = 1; k <= 4; ++k) {
+            for (size_t n : {(size_t) k, (size_t) 1000, (size_t) 4097, (size_t) 65536}) {
+                multi_wg_case<float, OR_SUM, OD_FLOAT>(teams, k, n, 256, sb, db, rc);
+                multi_wg_case<int32_t, OR_MIN, OD_INT32>(teams, k, n, 1024, sb, db, rc);
+                multi_wg_case<double, OR_PROD, OD_DOUBLE>(teams, k, n, 128, sb, db, rc);
+                multi_wg_case<uint64_t, OR_XOR, OD_UINT64>(teams, k, n, 64, sb, db, rc);
+            }
+        }
+        for (int g = 0; g < 4; ++g)
+            if (teams.t[g] != ISHMEM_TEAM_INVALID) ishmem_team_destroy(teams.t[g]);
     }
     // fcollect / collect / inscan / exscan from inside a kernel (dest room: npes * (n + 37 npes)).
     for (size_t n : {1, 5, 64, 1000, 4099}) {

@@ -8,6 +8,8 @@
 //   on_queue            ishmemx_long_sum_reduce_on_stream (the on_queue analogue), one sync
 //   device_grp1         ishmemx_long_sum_reduce_work_group from a user kernel, 1024-thread group
 //   device_subgroup     the same with one wavefront (sub_group analogue)
+//   device_multi_wg     1 / 2 / 4 / 8 work-groups of 1024 threads in one kernel, each reducing
+//                       nelems / groups elements on its own clone of TEAM_WORLD (groups column)
 // Every PE runs the same schedule; the iteration count is agreed with a max-reduce of the
 // durations (the reference broadcasts PE 0's command instead).
 // Launch: ISHMEM_PE / ISHMEM_NPES / ISHMEM_DEVICE / ISHMEM_BOOTSTRAP_KEY per process, or torchrun.
@@ -30,6 +32,23 @@ __global__ void wg_loop(long *dest, const long *src, size_t n,
     int bad = 0;
     for (size_t i = 0; i < iters; ++i) bad |= ishmemx_long_sum_reduce_work_group(dest, src, n, G());
     if (threadIdx.x == 0) *rc = bad;
+}
+
+// device_multi_wg (ishmem_tester.h:1344-1360): `groups` work-groups of one kernel, group g reducing
+// its slice [g * per, (g + 1) * per) on its own clone of TEAM_WORLD (:299-304).
+struct WgTeams {
+    int t[8];
+};
+
+__global__ void multi_wg_loop(WgTeams teams, long *dest, const long *src, size_t per,
+                              size_t iters, int *rc)
+{
+    const size_t off = (size_t) blockIdx.x * per;
+    int bad = 0;
+    for (size_t i = 0; i < iters; ++i)
+        bad |= ishmemx_long_sum_reduce_work_group(teams.t[blockIdx.x], dest + off, src + off, per,
+                                                  ishmemx_dev::work_group);
+    if (threadIdx.x == 0 && bad) *rc = bad;
 }
 
 static double now_s()
@@ -62,11 +81,25 @@ int main(int argc, char **argv)
     (void) hipMemset(src, 1, max_nelems * sizeof(long));
     if (csv && me == 0) printf("csv,testname,ipc,npes,type,op,mode,groups,threads,bytes,pe,latency_us,bw_mb\n");
 
-    const char *modes[] = {"host_device_device", "on_queue", "device_grp1", "device_subgroup"};
+    WgTeams teams{};
+    for (int g = 0; g < 8; ++g)
+        if (ishmem_team_split_strided(ISHMEM_TEAM_WORLD, 0, 1, npes, nullptr, 0, &teams.t[g]) != 0) {
+            fprintf(stderr, "team clone %d: %s\n", g, ishmemi_c_last_error());
+            return 1;
+        }
+    // (mode, groups): the multi-work-group mode at 1, 2, 4 and 8 groups of 1024 threads.
+    const struct {
+        const char *mode;
+        int groups;
+    } runs[] = {{"host_device_device", 1}, {"on_queue", 1},        {"device_grp1", 1},     {"device_subgroup", 1},
+                {"device_multi_wg", 1},    {"device_multi_wg", 2}, {"device_multi_wg", 4}, {"device_multi_wg", 8}};
     int failures = 0;
-    for (const char *mode : modes) {
+    for (const auto &rr : runs) {
+        const char *mode = rr.mode;
+        const int groups = rr.groups;
         const bool wave = !strcmp(mode, "device_subgroup"), grp = !strcmp(mode, "device_grp1");
-        for (size_t n = 1; n <= max_nelems; n <<= 1) {
+        const bool multi = !strcmp(mode, "device_multi_wg");
+        for (size_t n = multi ? (size_t) groups : 1; n <= max_nelems; n <<= 1) {
             auto run = [&](size_t iters) -> double {
                 ishmem_barrier_all();
                 const double t0 = now_s();
@@ -77,6 +110,14 @@ int main(int argc, char **argv)
                     for (size_t i = 0; i < iters; ++i)
                         failures += ishmemx_long_sum_reduce_on_stream(dst, src, n, nullptr, st) != 0;
                     (void) hipStreamSynchronize(st);
+                } else if (multi) {
+                    (void) hipMemset(rc, 0, sizeof(int));
+                    hipLaunchKernelGGL(multi_wg_loop, dim3(groups), dim3(1024), 0, st, teams, dst, (const long *) src,
+                                       n / (size_t) groups, iters, rc);
+                    (void) hipStreamSynchronize(st);
+                    int r = 0;
+                    (void) hipMemcpy(&r, rc, sizeof(int), hipMemcpyDeviceToHost);
+                    failures += r != 0;
                 } else {
                     if (wave)
                         hipLaunchKernelGGL(wg_loop<ishmemx_dev::wavefront_t>, dim3(1), dim3(64), 0, st,
@@ -110,13 +151,13 @@ int main(int argc, char **argv)
             if (tested && me == 0) {
                 const double lat = dur / (double) iters * 1e6;
                 const double bw = (double) sizeof(long) * (double) n * (double) iters / (dur * 1e6);
-                const size_t threads = grp ? 1024 : wave ? 64 : 1;
+                const size_t threads = (grp || multi) ? 1024 : wave ? 64 : 1;
                 if (csv)
-                    printf("csv,reduce_bw,1,%d,long,sum,%s,1,%zu,%zu,%s,%f,%f\n", npes, mode, threads, n,
+                    printf("csv,reduce_bw,1,%d,long,sum,%s,%d,%zu,%zu,%s,%f,%f\n", npes, mode, groups, threads, n,
                            npes > 1 ? "xe" : "self", lat, bw);
                 else
-                    printf("test reduce_bw n_pes %d type long op sum mode %s threads %zu nelems %zu "
-                           "latency %f us bw %f MB/s\n", npes, mode, threads, n, lat, bw);
+                    printf("test reduce_bw n_pes %d type long op sum mode %s groups %d threads %zu nelems %zu "
+                           "latency %f us bw %f MB/s\n", npes, mode, groups, threads, n, lat, bw);
                 fflush(stdout);
             }
         }
@@ -129,6 +170,7 @@ int main(int argc, char **argv)
     for (size_t i = 0; i < max_nelems; ++i) wrong += (unsigned long) host[i] != want;
     free(host);
     if (me == 0) printf("%s errors %d wrong %zu\n", (failures || wrong) ? "FAIL" : "PASS", failures, wrong);
+    for (int g = 0; g < 8; ++g) ishmem_team_destroy(teams.t[g]);
     (void) hipFree(rc);
     (void) hipStreamDestroy(st);
     ishmem_free(agree);

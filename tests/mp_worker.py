@@ -106,8 +106,8 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             ish.ishmem_free(s_)
 
         if "phasedparam" in scenarios:
-            # The phased threshold agreed at init: the maximum over the PEs, off by default when
-            # more than 4 PEs share a device unless some PE set ISHMEM_PHASED_MIN_BYTES.
+            # The phased threshold agreed at init: the maximum over the PEs (16 MiB by default,
+            # whatever the topology; -1 on any PE turns it off).
             want = int(os.environ["PHASED_WANT"])
             if int(ish.get_param("phased_min_bytes")) != want:
                 fails.append(f"pe{pe} phased_min_bytes {ish.get_param('phased_min_bytes')} != agreed {want}")
@@ -474,6 +474,30 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 if not _bits_equal(hip.download(sc, n_big, np.int32), ref):
                     fails.append(f"pe{pe} graph inscan {rep} wrong")
             del g
+            # Pageable host buffers (malloc'd numpy, 2 MiB: above the 1 MiB page-locking threshold)
+            # in a captured on-stream reduce: the library must not page-lock them for
+            # the call under capture — its synchronize would invalidate the capture and the pages
+            # would be unlocked before any replay.  The captured staged copies replay correctly.
+            n_h = (2 << 20) // 4
+            hsrc, hdst = np.zeros(n_h, np.float32), np.zeros(n_h, np.float32)
+            ish.ishmem_barrier_all()
+            with hip.Graph(st_) as g2:
+                rc_cap = ish.ishmemx_float_sum_reduce_on_stream(hdst.ctypes.data, hsrc.ctypes.data, n_h, ret, st_)
+            if rc_cap:
+                fails.append(f"pe{pe} graph pageable: captured call failed: {ish.last_error()}")
+            else:
+                for rep in range(3):
+                    vals = [oracle.fill_random(DT["float"], 990 + 10 * rep + j, n_h) for j in range(npes)]
+                    hsrc[:] = vals[pe]
+                    hdst[:] = 0
+                    hip.memset(ret, 0xFF, 4)
+                    ish.ishmem_barrier_all()
+                    g2.launch()
+                    hip.stream_synchronize(st_)
+                    if int(hip.download(ret, 1, np.int32)[0]) != 0:
+                        fails.append(f"pe{pe} graph pageable replay {rep}: ret != 0")
+                    check(f"graph pageable {rep}", OPS["sum"], DT["float"], vals, hdst.copy())
+            del g2
             hip.stream_destroy(st_)
             for b_ in (s1, d1, s2, d2, fc, sc, ret):
                 ish.ishmem_free(b_)
@@ -699,6 +723,60 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                     fails.append(f"pe{pe} huge: {bad} of {4 * n} bytes wrong")
             ish.ishmem_free(d_base)
             ish.ishmem_free(s_base)
+
+        if "opposite" in scenarios:
+            # two teams with the same members (two clones of WORLD), one
+            # collective each on its own stream, issued in OPPOSITE orders on the two halves of the
+            # PEs with a 20 ms pause between the two issues, so the first-issued kernels already wait
+            # for their peers when the second ones are enqueued.  Run with every PE on its own
+            # (emulated) device: round 3 sized each persistent / LL grid for the whole device, so the
+            # first-issued launches held every CU while waiting for kernels that then could not
+            # become resident (device timeouts).  The waiting footprint (kernels.h) keeps each such
+            # launch to 1 / wait_slots of the device.  LL (64 KiB), persistent (1, 4 MiB), phased
+            # (32 MiB); results checked, and no call may take seconds.
+            r1, ta = ish.ishmem_team_split_strided(ish.ISHMEM_TEAM_WORLD, 0, 1, npes)
+            r2, tb = ish.ishmem_team_split_strided(ish.ISHMEM_TEAM_WORLD, 0, 1, npes)
+            if r1 or r2:
+                fails.append(f"pe{pe} opposite split: {ish.last_error()}")
+            else:
+                first = pe < max(1, npes // 2)
+                nmax = 8 << 20
+                sa, da, sb, db = (heap(nmax, DT["float"]) for _ in range(4))
+                ret = ish.ishmem_malloc(8)
+                sts = [hip.stream_create() for _ in range(2)]
+                for n in (1 << 14, 1 << 18, 1 << 20, 8 << 20):
+                    for rnd in range(2):
+                        a = [oracle.fill_random(DT["float"], 0x5A00 + 64 * rnd + j, n) for j in range(npes)]
+                        b = [oracle.fill_random(DT["float"], 0x5B00 + 64 * rnd + j, n) for j in range(npes)]
+                        hip.upload(sa, a[pe])
+                        hip.upload(sb, b[pe])
+                        hip.memset(ret, 0x7F, 8)
+                        ish.ishmem_barrier_all()
+                        calls = [(da, sa, ret, sts[0], ta), (db, sb, ret + 4, sts[1], tb)]
+                        if not first:
+                            calls.reverse()
+                        t0 = time.monotonic()
+                        rc = [ish.reduce_on_stream("sum", "float", calls[0][0], calls[0][1], n, *calls[0][2:])]
+                        time.sleep(0.02)
+                        rc.append(ish.reduce_on_stream("sum", "float", calls[1][0], calls[1][1], n, *calls[1][2:]))
+                        for st_ in sts:
+                            hip.stream_synchronize(st_)
+                        dt_s = time.monotonic() - t0
+                        rets = hip.download(ret, 2, np.int32)
+                        if any(rc) or np.any(rets != 0) or dt_s > 5.0:
+                            fails.append(f"pe{pe} opposite n={n} round {rnd}: rc={rc} ret={rets} {dt_s:.2f} s "
+                                         f"{ish.last_error()}")
+                            break
+                        check(f"opposite a n={n} {rnd}", OPS["sum"], DT["float"], a, hip.download(da, n, np.float32))
+                        check(f"opposite b n={n} {rnd}", OPS["sum"], DT["float"], b, hip.download(db, n, np.float32))
+                    if fails:
+                        break
+                for st_ in sts:
+                    hip.stream_destroy(st_)
+                for b_ in (ret, db, sb, da, sa):
+                    ish.ishmem_free(b_)
+                ish.ishmem_team_destroy(ta)
+                ish.ishmem_team_destroy(tb)
 
         if "concurrent" in scenarios and npes >= 4 and npes % 2 == 0:
             # Collectives of different teams in flight at once on different streams (the TP / DP

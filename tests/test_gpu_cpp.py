@@ -73,7 +73,8 @@ def test_device_api_program_builds():
 @pytest.mark.gpu
 @pytest.mark.parametrize("npes", [2, 3])
 def test_device_initiated_work_group_reduce(npes):
-    """ishmemx_*_reduce_work_group called from a user kernel (include/ishmemx_device.h)."""
+    """ishmemx_*_reduce_work_group called from a user kernel (include/ishmemx_device.h), including the
+    reference's device_multi_wg mode: k = 1..4 work-groups of one kernel on k clones of TEAM_WORLD."""
     run_exe(build_exe(ROOT / "tests/cpp/device_wg.hip", DEV_EXE), npes)
 
 
@@ -100,3 +101,6 @@ def test_reduce_bw_harness_runs_and_checks():
     assert all(p.returncode == 0 for p in procs), outs[0][-2000:] + outs[1][-2000:]
     assert "PASS errors 0" in outs[0]
     assert outs[0].count("csv,reduce_bw,") >= 4 * 8
+    # device_multi_wg (ishmem_tester.h:1344-1360): rows for 1, 2, 4 and 8 work-groups.
+    for groups in (1, 2, 4, 8):
+        assert f",device_multi_wg,{groups},1024," in outs[0], outs[0][-2000:]

@@ -107,11 +107,12 @@ def test_launch_parameters_agreed_at_init():
 @pytest.mark.parametrize("case", ["p2_default", "p8_default", "p8_one_pe_explicit", "p3_one_pe_off"])
 def test_phased_threshold_agreed_at_init(case):
     # Every PE must take the same path (the phased path's barriers are separate launches): the
-    # threshold is the maximum over the PEs; by default 16 MiB, off when more than 4 PEs share a
-    # GPU (time-sliced barriers) unless a PE set ISHMEM_PHASED_MIN_BYTES; -1 on any PE disables it.
+    # threshold is the maximum over the PEs; by default 16 MiB whatever the topology (round 3
+    # turned it off when more than 4 PEs shared a GPU; round 4 runs co-located PEs on the node's
+    # path); -1 on any PE disables it.
     npes, env, want = {
         "p2_default": (2, {}, 16 << 20),
-        "p8_default": (8, {}, -1),
+        "p8_default": (8, {}, 16 << 20),
         "p8_one_pe_explicit": (8, {"ISHMEM_PHASED_MIN_BYTES": ["64M"] + [""] * 7}, 64 << 20),  # K / M / G suffixes
         "p3_one_pe_off": (3, {"ISHMEM_PHASED_MIN_BYTES": ["", "-1", ""]}, -1),
     }[case]
@@ -176,17 +177,28 @@ def test_phased_paths_on_teams_streams_and_staged_buffers(npes, scenarios):
 @pytest.mark.parametrize("npes", [2, 8])
 def test_one_pe_per_gpu_configuration_emulated(npes):
     # The 8-GPU node's path choices, rehearsed on the one GPU: every PE reports its own device
-    # (ISHMEM_TEST_PCI_BUS), so the device share is 1 and the phased default is on at every team
-    # size (16 MiB), while the PEs still share one GPU.  Golden inputs, in place, edges, 256 / 64 MiB
-    # in full, hipGraph replay and the tripwire must all hold.  The grid cap keeps all PEs' grids
-    # resident together: with share 1 each PE would size its persistent grid for the whole GPU, and
-    # eight such grids on one device let one PE's waiting workgroups hold every CU a peer needs to
-    # announce (measured: device timeouts in the tripwire) — the co-location hazard the share-based
-    # split prevents, which one PE per GPU cannot meet.
-    env = {"ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 768 // npes,
+    # (ISHMEM_TEST_PCI_BUS), so the device share is 1, while the PEs still share one GPU.  Golden
+    # inputs, in place, edges, 256 / 64 MiB in full, hipGraph replay and the tripwire must all hold,
+    # with the grid cap lifted (ISHMEM_MAX_BLOCKS 1024).  Round 3 had to cap it at 768 / npes: each
+    # PE sized its persistent grid for the whole GPU, and eight such waiting grids on one device
+    # timed out in the tripwire (profiles/r03/phased_share/r03zh_*).  Now every waiting launch takes
+    # at most 1 / wait_slots of the device (kernels.h, "Waiting footprint"), so eight fit at once.
+    env = {"ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
            "ISHMEM_PHASED_MIN_BYTES": "", "PHASED_WANT": 16 << 20}
     run_pes(npes, ["phasedparam", "golden", "inplace", "edge", "large", "graph", "tripwire"], env=env,
             timeout=400)
+
+
+@pytest.mark.parametrize("npes,slots", [(2, 16), (4, 16), (8, 32)])
+def test_opposite_order_collectives_of_two_teams_one_pe_per_gpu_emulated(npes, slots):
+    # collectives of two teams on two streams, issued in opposite orders on the
+    # two halves of the PEs, each PE on its own (emulated) device and no grid cap — LL, persistent
+    # (1 / 4 MiB) and phased sizes.  Deadlock-free by construction while the co-located PEs' waiting
+    # launches fit the device: 2 per PE here, so 8 co-located PEs need 1/32 each (ISHMEM_WAIT_SLOTS);
+    # one PE per GPU (4 hardware queues per process) is covered by the default 16.
+    env = {"ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
+           "ISHMEM_PHASED_MIN_BYTES": "", "ISHMEM_WAIT_SLOTS": slots}
+    run_pes(npes, ["opposite"], env=env, timeout=300)
 
 
 @pytest.mark.parametrize("path", ["phased", "persistent"])
@@ -208,10 +220,15 @@ def test_coherence_tripwire_chained_producer_reduce(npes):
     run_pes(npes, ["tripwire"], env={"ISHMEM_MAX_BLOCKS": 1024}, timeout=300)
 
 
-def test_config4_eight_pes_1GiB_f32_sum_full_compare():
-    # BASELINE configs[3] at its size on the one GPU: 8 PEs x 1 GiB, full default grid per PE
-    # (8 x 1024 workgroups oversubscribe the device: residency-independent protocol).
-    run_pes(8, ["cfg4"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "3G"}, timeout=600)
+@pytest.mark.parametrize("path", ["phased", "persistent"])
+def test_config4_eight_pes_1GiB_f32_sum_full_compare(path):
+    # BASELINE configs[3] at its size on the one GPU: 8 PEs x 1 GiB, every word compared.  "phased"
+    # sets ISHMEM_PHASED_MIN_BYTES=16M on every PE — the path one PE per GPU takes on the node
+    # (rs_phase_kernel<P=8> + ag_phase_kernel; also the default now); "persistent" pins the
+    # persistent kernel.
+    env = {"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "3G",
+           "ISHMEM_PHASED_MIN_BYTES": "16M" if path == "phased" else -1}
+    run_pes(8, ["cfg4"], env=env, timeout=600)
 
 
 @pytest.mark.parametrize("oneshot", ["default", "rs_ag"])
@@ -235,8 +252,10 @@ def test_config1_two_pes_int32_sum_host_buffers():
 def test_config5_min_max_prod_int32_f64_4KiB_to_4GiB(npes):
     # BASELINE configs[4]: min/max/prod x int32/float64, 4 KiB * 4^k up to 4 GiB per PE, every
     # chunk edge checked (4 GiB src + 4 GiB dest + staging per PE: a 9 GiB heap).
+    # ISHMEM_PHASED_MIN_BYTES=16M on every PE: from 16 MiB the node's path (rs_phase_kernel<P> +
+    # ag_phase_kernel), up to 4 GiB per PE — past 2^32 bytes of payload per PE.
     run_pes(npes, ["cfg5"], env={"ISHMEM_MAX_BLOCKS": 1024, "ISHMEM_SYMMETRIC_SIZE": "9G",
-                                 "CFG5_MAX_BYTES": 4 << 30}, timeout=900)
+                                 "ISHMEM_PHASED_MIN_BYTES": "16M", "CFG5_MAX_BYTES": 4 << 30}, timeout=900)
 
 
 @pytest.mark.parametrize("npes", [2, 3, 4, 8])

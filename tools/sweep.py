@@ -25,6 +25,8 @@ def main() -> None:
     ap.add_argument("--factor", type=int, default=4)
     ap.add_argument("--coll", choices=["reduce", "fcollect", "inscan"], default="reduce")
     ap.add_argument("--graph", action="store_true", help="time a hipGraph of --iters captured calls")
+    ap.add_argument("--emulate-share1", action="store_true",
+                    help="every PE reports its own device (ISHMEM_TEST_PCI_BUS): the launch shapes of one PE per GPU")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -38,6 +40,8 @@ def main() -> None:
         obj = [key]
         dist.broadcast_object_list(obj, src=0)
         key = obj[0]
+    if args.emulate_share1:
+        os.environ["ISHMEM_TEST_PCI_BUS"] = f"fake-bus-{rank}"
     import ishmem_amd as ish
     from ishmem_amd import hip
     dev = 0 if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else local
@@ -49,7 +53,8 @@ def main() -> None:
     st = hip.stream_create()
     if rank == 0:
         print(f"# coll={args.coll} graph={args.graph} pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
-              f"ll_max_bytes={ish.get_param('ll_max_bytes')}")
+              f"ll_max_bytes={ish.get_param('ll_max_bytes')} wait_slots={ish.get_param('wait_slots')} "
+              f"device_share={ish.get_param('device_share')}")
         print("bytes,us_per_call,algbw_GiBps,ok")
     def call(n):
         if args.coll == "fcollect":
