@@ -289,8 +289,8 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
       wait  - the persistent kernel (phased path off) at 1 / 4 / 16 MiB with wait_slots 4 / 8 / 16 /
               32: each waiting launch may hold 1 / wait_slots of the device (kernels.h, "Waiting
               footprint"; 16 = 64 workgroups is the default) — whether that grid fills the links;
-      phased - 4 / 16 / 64 MiB and the payload on the phased path (one-shot grids between
-               barriers) and on the persistent kernel (the phased threshold);
+      phased - 2 / 4 / 8 / 16 / 64 MiB and the payload on the phased path (one-shot grids
+               between barriers) and on the persistent kernel (the phased threshold, 4 MiB);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
       ll    - 4 / 16 / 64 KiB with the one-hop granule path on (default) and off."""
 
@@ -330,7 +330,7 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
         for nb in (1 << 20, 4 << 20, 16 << 20):
             if nb <= B:
                 run("wait", "wait_slots", ws, nb, 20, also={"phased_min_bytes": -1})
-    for nb in sorted({4 << 20, 16 << 20, 64 << 20, B}):
+    for nb in sorted({2 << 20, 4 << 20, 8 << 20, 16 << 20, 64 << 20, B}):
         if nb <= B:
             run("phased", "phased_min_bytes", 0, nb, 5 if nb == B else 20)
             run("persistent", "phased_min_bytes", -1, nb, 5 if nb == B else 20)

@@ -134,11 +134,17 @@ struct Team {
 };
 
 constexpr long long kPhasedOff = std::numeric_limits<long long>::max();
-// Measured (profiles/r03/phased/, profiles/r03/paths/): 2 PEs x 1 GiB 0.84 ms phased
-// against 0.99-1.13 ms persistent; 2 PEs x 32 / 64 MiB 36 / 59 us against the two-member one-shot
-// fold's 42 / 78 us; 4 PEs x 16 MiB 40 vs 48 us; at 8 MiB and below the extra barrier round trips
-// cost what the one-shot grids save.
-constexpr long long kPhasedDefault = 16ll << 20;
+// Round 3 put the threshold at 16 MiB: 2 PEs x 1 GiB 0.84 ms phased against 0.99-1.13 ms
+// persistent; 2 PEs x 32 / 64 MiB 36 / 59 us against the two-member one-shot fold's 42 / 78 us;
+// 4 PEs x 16 MiB 40 vs 48 us.  Round 4 caps the persistent kernel's grid (it waits for peers, so
+// it may hold at most 1 / wait_slots of the device, kernels.h) and lowers the threshold to 4 MiB,
+// where the phased path's never-waiting full-device grids overtake the capped grid
+// (profiles/r04/wait_cost/: 2 PEs with one-PE-per-GPU shapes, 4 / 8 MiB 16.6-17.3 / 19.2-20.1 us
+// phased against 20.5-20.7 / 33.8-34.0 us persistent, 2 MiB 16-17 against 14.1-14.3 us).  Over
+// xGMI the same crossover follows from the links: a 64-workgroup grid keeps ~1 MiB of peer loads
+// in flight, near the 7 links' bandwidth-delay product, while the three barriers cost a few fabric
+// round trips; the N > 1 bench line's xgmi_tuning leg records both paths at 2-64 MiB.
+constexpr long long kPhasedDefault = 4ll << 20;
 // Round 3 turned it off when more than 4 PEs shared one GPU (co-located rehearsals, where the
 // three barrier launches cost ~40-80 us each among eight time-sliced processes).  Round 4 drops
 // that rule: co-located runs take the path one PE per GPU takes, so the 8-PE tests at BASELINE's

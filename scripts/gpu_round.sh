@@ -42,6 +42,15 @@ for s in $STEPS; do
             ISHMEM_BENCH_SAME_DEVICE=1 run bench_$s 900 python bench.py --gpus $np_ --steps 10 --warmup 3 \
                 --mib ${MIB:-1024} --sweep-max-mib ${SWEEP_MIB:-4096} ;;
     sweep1) run sweep1 300 python tools/sweep.py --max-mib 1024 ;;
+    bw2)    # tests/cpp/reduce_bw.cpp at 2 PEs (all modes incl. device_multi_wg 1/2/4/8 groups), CSV
+            key=bw$RANDOM$RANDOM
+            for pe in 0 1; do
+              ISHMEM_PE=$pe ISHMEM_NPES=2 ISHMEM_DEVICE=0 ISHMEM_BOOTSTRAP_KEY=$key ISHMEM_SYMMETRIC_SIZE=1G \
+                timeout -k 10 600 build/reduce_bw --csv -m ${BW_MAX:-1048576} > "$OUT/reduce_bw_p2_pe$pe.csv" 2>&1 &
+            done
+            wait; rc=$?
+            echo "=== bw2 rc=$rc" | tee -a "$OUT/steps.log"; tail -3 "$OUT/reduce_bw_p2_pe0.csv"
+            if fatal $rc; then exit $rc; fi ;;
     sweep2|sweep4|sweep8) np_=${s#sweep}
             ISHMEM_BENCH_SAME_DEVICE=1 run $s 600 python -m torch.distributed.run \
                 --nnodes=1 --nproc-per-node $np_ --master-addr 127.0.0.1 --master-port 2951$np_ tools/sweep.py --max-mib 256 ;;

@@ -107,12 +107,12 @@ def test_launch_parameters_agreed_at_init():
 @pytest.mark.parametrize("case", ["p2_default", "p8_default", "p8_one_pe_explicit", "p3_one_pe_off"])
 def test_phased_threshold_agreed_at_init(case):
     # Every PE must take the same path (the phased path's barriers are separate launches): the
-    # threshold is the maximum over the PEs; by default 16 MiB whatever the topology (round 3
+    # threshold is the maximum over the PEs; by default 4 MiB whatever the topology (round 3
     # turned it off when more than 4 PEs shared a GPU; round 4 runs co-located PEs on the node's
     # path); -1 on any PE disables it.
     npes, env, want = {
-        "p2_default": (2, {}, 16 << 20),
-        "p8_default": (8, {}, 16 << 20),
+        "p2_default": (2, {}, 4 << 20),
+        "p8_default": (8, {}, 4 << 20),
         "p8_one_pe_explicit": (8, {"ISHMEM_PHASED_MIN_BYTES": ["64M"] + [""] * 7}, 64 << 20),  # K / M / G suffixes
         "p3_one_pe_off": (3, {"ISHMEM_PHASED_MIN_BYTES": ["", "-1", ""]}, -1),
     }[case]
@@ -184,7 +184,7 @@ def test_one_pe_per_gpu_configuration_emulated(npes):
     # timed out in the tripwire (profiles/r03/phased_share/r03zh_*).  Now every waiting launch takes
     # at most 1 / wait_slots of the device (kernels.h, "Waiting footprint"), so eight fit at once.
     env = {"ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
-           "ISHMEM_PHASED_MIN_BYTES": "", "PHASED_WANT": 16 << 20}
+           "ISHMEM_PHASED_MIN_BYTES": "", "PHASED_WANT": 4 << 20}
     run_pes(npes, ["phasedparam", "golden", "inplace", "edge", "large", "graph", "tripwire"], env=env,
             timeout=400)
 
