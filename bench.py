@@ -891,7 +891,11 @@ def main() -> int:
             "config": {"workload": f"float32 sum-reduce, {B / 2**20:g} MiB per PE, {world} PE(s), "
                                    f"symmetric-heap device buffers", "nreduce": n,
                        "bytes_per_pe": B, "pes": world,
-                       "parallelism": "1 PE self-reduce" if world == 1 else f"direct RS+AG over {world} PEs"},
+                       "parallelism": "1 PE self-reduce" if world == 1 else f"direct RS+AG over {world} PEs",
+                       **({"semantics": "a 1-PE reduce is a copy in the reference (reduce_impl.h:288-289): the "
+                                        "timed kernel moves 2 B per payload byte and does no f32 arithmetic; the "
+                                        "f32 sum itself is timed in 'combine' (dst = a + b, 3 B per payload byte)"}
+                          if world == 1 else {})},
             "kernel_ms": kern_ms, "checked": checked, "targets": targets,
             **({"flag_memory": flag_memory} if world > 1 else {}),
             **({"topology": link_topology(hip, device, world)} if world > 1 and not same_device else {}),

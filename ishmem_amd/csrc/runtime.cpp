@@ -36,6 +36,8 @@ constexpr size_t kDevFlagBytes = (size_t) kMaxTeams * kDevFlagWordsPerTeam * 4;
 constexpr size_t kLLOffset = ((size_t) kMaxTeams * kTeamFlagBytes + kDevFlagBytes + 255) & ~(size_t) 255;
 constexpr size_t kFlagAllocBytes = kLLOffset + (size_t) kMaxTeams * kLLTeamBytes;
 constexpr size_t kHeapAlign = 256;
+// Offset of team_exchange's arrays in the host-mapped error-word allocation (after the words).
+constexpr size_t kErrExchOffset = ((kMaxTeams + 1) * sizeof(uint32_t) + 63) & ~(size_t) 63;
 constexpr size_t kLargeAllocBytes = (size_t) 1 << 20, kLargeAlign = (size_t) 2 << 20;
 // Slots of the host-memory pipeline (reduce_staged): chunk k uses slot k mod slots.  More slots
 // shorten the pipeline's fill and drain (a chunk is staging / slots bytes) and give copy-in more
@@ -181,6 +183,8 @@ struct State {
     uint32_t *peer_flags[kMaxPes] = {};
     uint32_t *err_host = nullptr;  // host-mapped error words, one per team (+1: device API)
     uint32_t *err_dev = nullptr;
+    // Host-mapped coherent [2][kMaxPes] u64 (same allocation as err_host): team_exchange's arrays.
+    uint64_t *exch_host = nullptr, *exch_dev = nullptr;
     ishmemi_c_device_ctx_t *dctx = nullptr;  // device copy of the device-API context
     uint32_t *dev_epochs = nullptr;
     uint32_t *kern_ep = nullptr;  // [team][kEpTeamWords] launch words of the host-launched kernels
@@ -956,9 +960,19 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
 // anything that must match across members is launched (a member that failed alone would leave
 // its peers waiting for launches that never come).  Called without the state lock.
 constexpr uint64_t kAgreeStaged = 1ull << 62, kAgreeFail = 1ull << 63;
+bool member_call(const State &s, int team);
+
+// The agreement step of the blocking fcollect / collect / scan / broadcast (staged path, counts,
+// argument failures): an allgather of one u64 per member, before anything else is launched.
+// One small-message (LL) launch on a host-mapped coherent array: member i's word sits in slot i,
+// zeros elsewhere, so a uint64 SUM over the team is the allgather, read by the host once the
+// launch completes — no copy in or out.  Round 3 used a synchronous H2D copy, a whole fcollect
+// launch (start and done handshakes) and a synchronous D2H copy (the exchange roughly
+// doubled a small blocking fcollect / scan; BASELINE.md round 4 has the before / after).
 int team_exchange(int team, uint64_t mine, uint64_t *all)
 {
     State &s = S();
+#ifdef ISHMEMI_EXCHANGE_VIA_FCOLLECT  // round-3 exchange (A/B builds only)
     const int p = s.teams[team].size;
     if (hipMemcpy(s.team_scratch, &mine, 8, hipMemcpyHostToDevice) != hipSuccess)
         return fail("team exchange: copy failed");
@@ -966,6 +980,29 @@ int team_exchange(int team, uint64_t mine, uint64_t *all)
     if (hipMemcpy(all, s.team_scratch + 64, 8 * (size_t) p, hipMemcpyDeviceToHost) != hipSuccess)
         return fail("team exchange: copy failed");
     return 0;
+#else
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!member_call(s, team)) return fail("team exchange: invalid team or caller not a member");
+    const Team &t = s.teams[team];
+    const int p = t.size;
+    volatile uint64_t *src = s.exch_host, *dst = s.exch_host + kMaxPes;
+    for (int j = 0; j < p; ++j) {
+        src[j] = j == t.my_idx ? mine : 0;
+        dst[j] = 0;
+    }
+    if (p > 1) {
+        if (reduce_ll(s, team, ISHMEMI_OP_SUM, ISHMEMI_DT_UINT64, s.exch_dev + kMaxPes, s.exch_dev, 8 * (size_t) p,
+                      nullptr, 0))
+            return 1;
+        if (mark_stream(s, 0)) return 1;
+        HIP_TRY(hipStreamSynchronize(0));
+        if (check_team_errors(s, team)) return 1;
+    } else {
+        dst[0] = mine;
+    }
+    for (int j = 0; j < p; ++j) all[j] = dst[j];
+    return 0;
+#endif
 }
 
 bool member_call(const State &s, int team)
@@ -1265,10 +1302,12 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     hipIpcMemHandle_t flags_handle{};
     const int first_kind = (int) std::min<long long>(kFlagsCoarse, std::max<long long>(0, env_ll("ISHMEM_FLAGS_KIND", 0)));
     if (alloc_flags(s, first_kind, npes > 1, &flags_handle)) return 1;
-    HIP_TRY(hipHostMalloc((void **) &s.err_host, (kMaxTeams + 1) * sizeof(uint32_t),
+    HIP_TRY(hipHostMalloc((void **) &s.err_host, kErrExchOffset + 2 * kMaxPes * sizeof(uint64_t),
                           hipHostMallocMapped | hipHostMallocCoherent));
-    memset(s.err_host, 0, (kMaxTeams + 1) * sizeof(uint32_t));
+    memset(s.err_host, 0, kErrExchOffset + 2 * kMaxPes * sizeof(uint64_t));
     HIP_TRY(hipHostGetDevicePointer((void **) &s.err_dev, s.err_host, 0));
+    s.exch_host = (uint64_t *) ((char *) s.err_host + kErrExchOffset);
+    s.exch_dev = (uint64_t *) ((char *) s.err_dev + kErrExchOffset);
     HIP_TRY(hipDeviceSynchronize());
 
     for (int i = 0; i < kMaxPes; ++i) {
@@ -1693,6 +1732,7 @@ int ishmemi_c_finalize(void)
     s.heap = nullptr;
     s.flags = nullptr;
     s.err_host = s.err_dev = nullptr;
+    s.exch_host = s.exch_dev = nullptr;
     s.initialized = false;
     return 0;
 }

@@ -25,6 +25,9 @@ def main() -> None:
     ap.add_argument("--factor", type=int, default=4)
     ap.add_argument("--coll", choices=["reduce", "fcollect", "inscan"], default="reduce")
     ap.add_argument("--graph", action="store_true", help="time a hipGraph of --iters captured calls")
+    ap.add_argument("--blocking", action="store_true",
+                    help="blocking host calls (ishmem_fcollectmem / ishmem_float_sum_inscan / ishmem_float_sum_reduce), "
+                         "timed on the host clock")
     ap.add_argument("--emulate-share1", action="store_true",
                     help="every PE reports its own device (ISHMEM_TEST_PCI_BUS): the launch shapes of one PE per GPU")
     args = ap.parse_args()
@@ -52,11 +55,17 @@ def main() -> None:
     hip.upload(src, (np.arange(nmax, dtype=np.int64) % 1024).astype(np.float32) + np.float32(rank))
     st = hip.stream_create()
     if rank == 0:
-        print(f"# coll={args.coll} graph={args.graph} pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
+        print(f"# coll={args.coll} graph={args.graph} blocking={args.blocking} pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
               f"ll_max_bytes={ish.get_param('ll_max_bytes')} wait_slots={ish.get_param('wait_slots')} "
               f"device_share={ish.get_param('device_share')}")
         print("bytes,us_per_call,algbw_GiBps,ok")
     def call(n):
+        if args.blocking:
+            if args.coll == "fcollect":
+                return ish.ishmem_fcollectmem(dst, src, n * 4)
+            if args.coll == "inscan":
+                return ish.lib().ishmemi_c_scan(0, ish.DTYPES["float"], 1, dst, src, n)
+            return ish.ishmem_float_sum_reduce(dst, src, n)
         if args.coll == "fcollect":
             return ish.fcollect_on_stream(dst, src, n * 4, 0, st)
         if args.coll == "inscan":
@@ -92,6 +101,13 @@ def main() -> None:
             e0.record(st)
             g.launch()
             e1.record(st)
+        elif args.blocking:
+            import time
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                if call(n):
+                    raise RuntimeError(ish.last_error())
+            host_us = (time.perf_counter() - t0) * 1e6 / iters
         else:
             e0.record(st)
             for _ in range(iters):
@@ -99,7 +115,7 @@ def main() -> None:
                     raise RuntimeError(ish.last_error())
             e1.record(st)
         hip.stream_synchronize(st)
-        us = e0.elapsed_ms(e1) * 1000.0 / iters
+        us = host_us if args.blocking else e0.elapsed_ms(e1) * 1000.0 / iters
         if dist is not None:
             t = torch.tensor([us], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
