@@ -43,6 +43,7 @@ constexpr size_t kLargeAllocBytes = (size_t) 1 << 20, kLargeAlign = (size_t) 2 <
 // shorten the pipeline's fill and drain (a chunk is staging / slots bytes) and give copy-in more
 // slack behind copy-out; ISHMEM_STAGING_SLOTS, agreed at init (the minimum), default 4.
 constexpr int kMaxStagingSlots = 8;
+constexpr int kStagedCopyKernelDefault = 0;
 
 thread_local std::string g_last_error;
 
@@ -213,6 +214,10 @@ struct State {
     hipEvent_t staging_ev = nullptr;
     bool staging_used = false;
     int staging_slots = 4;
+    // Host buffers the GPU can address (pinned / registered): copy chunks in (bit 1) / out (bit 0)
+    // of the staging region with the copy KERNEL instead of the DMA engines (ISHMEM_STAGED_COPY_KERNEL,
+    // set_param "staged_copy_kernel"; per PE, nothing is paired).
+    int staged_copy_kernel = 0;
     hipEvent_t ev_in[kMaxStagingSlots] = {}, ev_red[kMaxStagingSlots] = {}, ev_out[kMaxStagingSlots] = {};
 
     Team teams[kMaxTeams];
@@ -719,10 +724,24 @@ int reduce_staged(State &s, int team, int op, int dt, void *dst, const void *src
     return rc;
 }
 
+// Device address of host memory the GPU can load / store directly (hipHostMalloc'd, or registered
+// by the caller or by CallPins), else null.
+char *host_device_view(const void *p)
+{
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void) hipGetLastError();
+        return nullptr;
+    }
+    return attr.type == hipMemoryTypeHost ? (char *) attr.devicePointer : nullptr;
+}
+
 int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const void *src, size_t n,
                            int *ret, hipStream_t st)
 {
     const size_t es = dtype_size(dt);
+    const char *src_dev = (s.staged_copy_kernel & 2) ? host_device_view(src) : nullptr;
+    char *dst_dev = (s.staged_copy_kernel & 1) ? host_device_view(dst) : nullptr;
     const int nslots = s.staging_slots;
     const size_t slot_bytes = (s.staging_bytes / (size_t) nslots) & ~(kHeapAlign - 1);
     const size_t chunk = (slot_bytes / es) & ~size_t(63);
@@ -746,8 +765,11 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
         char *buf = s.staging + (size_t) sl * slot_bytes;
         const size_t m = std::min(chunk, n - off);
         if (used[sl]) HIP_TRY(hipStreamWaitEvent(s.copy_in, s.ev_out[sl], 0));  // slot drained
-        HIP_TRY(hipMemcpyAsync(buf, (const char *) src + off * es, m * es, hipMemcpyDefault,
-                               s.copy_in));
+        if (src_dev) {
+            if (launch_copy(buf, src_dev + off * es, m * es, s.copy_in)) return 1;
+        } else {
+            HIP_TRY(hipMemcpyAsync(buf, (const char *) src + off * es, m * es, hipMemcpyDefault, s.copy_in));
+        }
         HIP_TRY(hipEventRecord(s.ev_in[sl], s.copy_in));
         HIP_TRY(hipStreamWaitEvent(st, s.ev_in[sl], 0));
         // One PE: the in-place reduce of the staged chunk is the identity (reduce_impl.h:288-289).
@@ -759,7 +781,11 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
         }
         HIP_TRY(hipEventRecord(s.ev_red[sl], st));
         HIP_TRY(hipStreamWaitEvent(s.copy_out, s.ev_red[sl], 0));
-        HIP_TRY(hipMemcpyAsync((char *) dst + off * es, buf, m * es, hipMemcpyDefault, s.copy_out));
+        if (dst_dev) {
+            if (launch_copy(dst_dev + off * es, buf, m * es, s.copy_out)) return 1;
+        } else {
+            HIP_TRY(hipMemcpyAsync((char *) dst + off * es, buf, m * es, hipMemcpyDefault, s.copy_out));
+        }
         HIP_TRY(hipEventRecord(s.ev_out[sl], s.copy_out));
         used[sl] = true;
     }
@@ -1276,6 +1302,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.staging_bytes = (env_size("ISHMEM_STAGING_SIZE", (size_t) 128 << 20) + kHeapAlign - 1) &
                       ~(size_t) (kHeapAlign - 1);
     s.staging_slots = (int) std::min<long long>(kMaxStagingSlots, std::max<long long>(2, env_ll("ISHMEM_STAGING_SLOTS", 4)));
+    s.staged_copy_kernel = (int) (env_ll("ISHMEM_STAGED_COPY_KERNEL", kStagedCopyKernelDefault) & 3);
     const size_t heap_request = env_size("ISHMEM_SYMMETRIC_SIZE", (size_t) 4 << 30);
     if (!g_env_error.empty()) {
         const std::string e = g_env_error;
@@ -2391,6 +2418,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     std::lock_guard<std::mutex> lk(s.mu);
     const std::string n = name ? name : "";
     if (n == "max_blocks") s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, value));
+    else if (n == "staged_copy_kernel") s.staged_copy_kernel = (int) (value & 3);
     else if (n == "wait_slots") set_wait_slots((int) std::min<long long>(1 << 20, std::max<long long>(1, value)));
     else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
     else if (n == "stream_order") s.stream_order = value != 0;
@@ -2413,6 +2441,7 @@ long long ishmemi_c_get_param(const char *name)
     State &s = S();
     const std::string n = name ? name : "";
     if (n == "max_blocks") return s.max_blocks;
+    if (n == "staged_copy_kernel") return s.staged_copy_kernel;
     if (n == "wait_slots") return wait_slots();
     if (n == "timeout_ms") return s.timeout_ms;
     if (n == "stream_order") return s.stream_order ? 1 : 0;

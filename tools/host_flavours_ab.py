@@ -57,7 +57,8 @@ def main() -> None:
         return p.value, np.ctypeslib.as_array((ctypes.c_float * N).from_address(p.value))
 
     bufs = {}
-    for kind in ("hostmalloc", "hostmalloc_nc", "registered", "pageable"):
+    kinds = os.environ.get("AB_KINDS", "hostmalloc,hostmalloc_nc,registered,pageable").split(",")
+    for kind in kinds:
         pair = []
         for _ in range(2):
             if kind == "hostmalloc":
@@ -112,7 +113,7 @@ def main() -> None:
     if os.environ.get("AB_MODE") == "warmup":
         # Fresh buffers of each kind, then 10 single on-stream calls in a row: does the rate of
         # application-pinned buffers change with use (first DMA passes over new pages)?
-        for kind in ("hostmalloc", "registered", "pageable", "hostmalloc"):
+        for kind in [k for k in ("hostmalloc", "registered", "pageable", "hostmalloc") if k in bufs]:
             (ps, xs), (pd, xd) = bufs[kind]
             if kind.startswith("hostmalloc"):  # replace by fresh allocations
                 for p, _ in bufs[kind]:
@@ -140,7 +141,7 @@ def main() -> None:
             res[kind]["blocking"].append(round(blk, 2))
             res[kind]["on_stream"].append(round(ons, 2))
             res[kind]["dma_concurrent_GBps"].append(round(dm, 2))
-            print(json.dumps({"round": rnd, "kind": kind, "blocking_GiBps": round(blk, 2),
+            print(json.dumps({"round": rnd, "kind": kind, "staged_copy_kernel": int(ish.get_param("staged_copy_kernel")), "blocking_GiBps": round(blk, 2),
                               "on_stream_GiBps": round(ons, 2), "dma_concurrent_GBps": round(dm, 2),
                               "pipeline_each_way_GBps": round(ons * GiB / 1e9, 2), "checked": ok1 and ok2}),
                   flush=True)
