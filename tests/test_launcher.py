@@ -129,3 +129,34 @@ def test_cxx_ishmem_init_failure_exits_like_the_reference(tmp_path):
 def test_launch_info_is_declared_and_bound():
     L = _lib.load()
     assert L.ishmemi_c_launch_info.restype is ctypes.c_int
+
+
+ENV_PROBE = r'''
+import sys
+sys.path.insert(0, sys.argv[1])
+from ishmem_amd import _lib
+L = _lib.load(build_if_missing=False)
+rc = L.ishmemi_c_init_pe(0, 1, 0, b"envprobe")
+print("rc=%d|%s" % (rc, L.ishmemi_c_last_error().decode()))
+'''
+
+
+@pytest.mark.parametrize("name,value,bad", [
+    ("ISHMEM_PHASED_MIN_BYTES", "16MB x", True), ("ISHMEM_PHASED_MIN_BYTES", "abc", True),
+    ("ISHMEM_LL_MAX_BYTES", "64KQ", True), ("ISHMEM_SYMMETRIC_SIZE", "-4G", True),
+    ("ISHMEM_STAGING_SIZE", "nan", True), ("ISHMEM_PHASED_MIN_BYTES", "1e30", False),
+    ("ISHMEM_PHASED_MIN_BYTES", " 16MiB ", False), ("ISHMEM_LL_MAX_BYTES", "64kb", False),
+    ("ISHMEM_SYMMETRIC_SIZE", "2T", False), ("ISHMEM_PHASED_MIN_BYTES", "-1", False)])
+def test_byte_count_variables_parse_strictly(name, value, bad):
+    """ADVICE r03 (low): byte-count variables choose kernel paths every PE must agree on, so a typo
+    fails init with the variable named instead of parsing as something else; values past LLONG_MAX
+    clamp.  Checked before any GPU call (here the init then fails for want of a device, or not at
+    all on a GPU box — either way not on the variable)."""
+    out = subprocess.run([sys.executable, "-c", ENV_PROBE, str(ROOT)], env=clean_env(**{name: value}),
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    line = out.stdout.strip().splitlines()[-1]
+    if bad:
+        assert line.startswith("rc=1|") and name in line, line
+    else:
+        assert name not in line, line
