@@ -603,9 +603,17 @@ def e2e_leg(ish, hip, n, B, world, rank, dist, stream, barrier, steps, pinned: b
 
         def step_e2e():
             return ish.ishmemx_float_sum_reduce_on_stream(hd, hs, n, 0, stream)
-        if step_e2e() != 0:  # warm-up (creates the pipeline streams)
-            raise RuntimeError(ish.last_error())
-        hip.stream_synchronize(stream)
+        # Warm-up, each call timed: the first DMA passes over a process's newly pinned memory run
+        # slow (round 4, tools/host_flavours_ab.py AB_MODE=warmup: fresh hipHostMalloc buffers
+        # 20.9, 32.2, then 43.2 GiB/s per call), so the timed calls below are the steady state and
+        # the warm-up rates are reported beside them.
+        warm = []
+        for _ in range(3):
+            tw0 = time.perf_counter()
+            if step_e2e() != 0:
+                raise RuntimeError(ish.last_error())
+            hip.stream_synchronize(stream)
+            warm.append(round(max_over_ranks(dist, [time.perf_counter() - tw0])[0], 6))
         xd.fill(-1.0)  # the timed calls must write every word
         barrier()
         k = max(2, steps // 5)
@@ -626,6 +634,7 @@ def e2e_leg(ish, hip, n, B, world, rank, dist, stream, barrier, steps, pinned: b
         out = {"value": world * B / GiB / (te / k), "algbw_GiBps": B / GiB / (te / k),
                "unit": "GiB/s", "ms_per_step": te / k * 1000.0, "steps": k,
                "checked": bad == 0, "words_checked": n, "mode": "every word, every rank",
+               "warmup_GiBps_per_call": [round(B / GiB / t, 2) for t in warm],
                "buffers": "pinned host (hipHostMalloc)" if pinned else "pageable host (malloc'd numpy)",
                "pipeline": "H2D | reduce | D2H over 2 staging slots"}
         if pinned:
