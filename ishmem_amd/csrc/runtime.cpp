@@ -1288,7 +1288,11 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.pe = pe;
     s.npes = npes;
     set_device_share(1);
-    set_wait_slots((int) std::min<long long>(1 << 20, std::max<long long>(1, env_ll("ISHMEM_WAIT_SLOTS", kWaitSlotsDefault))));
+    // Default: 16, or 4 per hardware queue when the process was given more than 4 (GPU_MAX_HW_QUEUES):
+    // the cap must leave room for every kernel the process's queues can run at once (kernels.h).
+    const long long hwq = std::max<long long>(1, env_ll("GPU_MAX_HW_QUEUES", 4));
+    set_wait_slots((int) std::min<long long>(
+        1 << 20, std::max<long long>(1, env_ll("ISHMEM_WAIT_SLOTS", std::max<long long>(kWaitSlotsDefault, 4 * hwq)))));
     s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, env_ll("ISHMEM_MAX_BLOCKS", kMaxBlocks)));
     s.timeout_ms = std::max<long long>(1, env_ll("ISHMEM_TIMEOUT_MS", 60000));
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
