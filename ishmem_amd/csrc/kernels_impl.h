@@ -1131,7 +1131,6 @@ __device__ __forceinline__ uint64_t fold8(uint64_t acc, uint64_t x)
 
 // The grid is capped by the waiting footprint (resident_blocks_of), so a thread may own several
 // items (t, t + G*kBlock, ...): it pushes all of them before polling for any.
-template <typename T>
 __device__ __forceinline__ uint64_t ll_load(const LLArgs &a, uint64_t off, uint64_t valid)
 {
     if (valid == 8) return *(const uint64_t *) (a.src + off);
@@ -1154,7 +1153,7 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
     bool ok = true;
     for (uint64_t item = first; item < nitems; item += stride) {
         const uint64_t off = item * 8;
-        const uint64_t mine = ll_load<T>(a, off, a.nbytes - off < 8 ? a.nbytes - off : 8);
+        const uint64_t mine = ll_load(a, off, a.nbytes - off < 8 ? a.nbytes - off : 8);
         const uint64_t g0 = tag | (uint32_t) mine, g1 = tag | (uint32_t) (mine >> 32);
         for (int j = 0; j < p; ++j) {
             if (j == me) continue;
@@ -1167,7 +1166,7 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
     for (uint64_t item = first; item < nitems && ok; item += stride) {
         const uint64_t off = item * 8;
         const uint64_t valid = a.nbytes - off < 8 ? a.nbytes - off : 8;
-        const uint64_t mine = ll_load<T>(a, off, valid);
+        const uint64_t mine = ll_load(a, off, valid);
         uint64_t acc = 0;
         for (int j = 0; j < p && ok; ++j) {
             uint64_t x = mine;
@@ -1232,8 +1231,8 @@ using Canon = std::conditional_t<(OP == ISHMEMI_OP_MAX || OP == ISHMEMI_OP_MIN),
 // Grid cap of a kernel whose workgroups wait for peers (kernels.h, "Waiting footprint"): the
 // workgroups of `kernel` resident at once on this device (occupancy API, cached per kernel
 // address; it can over-report by one block per CU for SGPR-heavy kernels, MI355X_MICROARCH.md
-// residency, which the division leaves far from mattering) divided by share x wait_slots.  The collectives are
-// correct with any residency of their grid (owned work can be stolen, the rest is grabbed or
+// residency, which the division leaves far from mattering) divided by share x wait_slots.  The
+// collectives are correct with any residency of their grid (owned work can be stolen, the rest is grabbed or
 // strided; nothing is paired), so the cap only bounds how much of the device one waiting launch
 // can hold.  Round 3 sized the persistent reduce to the whole device (1024 workgroups, each
 // spinning at start): two collectives of different teams issued in opposite orders on two PEs
