@@ -586,8 +586,10 @@ def pcie_probe(hip, hs: int, hd: int, B: int, dist) -> dict:
 
 
 def e2e_leg(ish, hip, n, B, world, rank, dist, stream, barrier, steps, pinned: bool) -> dict:
-    """Host-memory end-to-end rate: ishmemx_float_sum_reduce_on_stream on host source / dest (the
-    reference's host path is reduce_impl.h:186-228, :301-315); every word of dest checked."""
+    """Host-memory end-to-end rate: the blocking ishmem_float_sum_reduce on host source / dest —
+    the reference's host path (reduce_impl.h:186-228, :301-315) is a blocking host call — each
+    call returning with dest final; every word of dest checked.  Also timed: the same calls
+    issued back to back on a stream (ishmemx_*_on_stream, one synchronize at the end)."""
     from ishmem_amd import selfcheck as sc
     try:
         if pinned:
@@ -602,6 +604,9 @@ def e2e_leg(ish, hip, n, B, world, rank, dist, stream, barrier, steps, pinned: b
             xs[lo:lo + m] = sc.pattern(rank, world, lo, m, np.float32)
 
         def step_e2e():
+            return ish.ishmem_float_sum_reduce(hd, hs, n)
+
+        def step_on_stream():
             return ish.ishmemx_float_sum_reduce_on_stream(hd, hs, n, 0, stream)
         # Warm-up, each call timed: the first DMA passes over a process's newly pinned memory run
         # slow (round 4, tools/host_flavours_ab.py AB_MODE=warmup: fresh hipHostMalloc buffers
@@ -614,9 +619,16 @@ def e2e_leg(ish, hip, n, B, world, rank, dist, stream, barrier, steps, pinned: b
                 raise RuntimeError(ish.last_error())
             hip.stream_synchronize(stream)
             warm.append(round(max_over_ranks(dist, [time.perf_counter() - tw0])[0], 6))
-        xd.fill(-1.0)  # the timed calls must write every word
-        barrier()
         k = max(2, steps // 5)
+        barrier()
+        ts0 = time.perf_counter()
+        for _ in range(k):
+            if step_on_stream() != 0:
+                raise RuntimeError(ish.last_error())
+        hip.stream_synchronize(stream)
+        ts = max_over_ranks(dist, [time.perf_counter() - ts0])[0]
+        xd.fill(-1.0)  # the timed blocking calls must write every word
+        barrier()
         te0 = time.perf_counter()
         for _ in range(k):
             if step_e2e() != 0:
@@ -635,8 +647,10 @@ def e2e_leg(ish, hip, n, B, world, rank, dist, stream, barrier, steps, pinned: b
                "unit": "GiB/s", "ms_per_step": te / k * 1000.0, "steps": k,
                "checked": bad == 0, "words_checked": n, "mode": "every word, every rank",
                "warmup_GiBps_per_call": [round(B / GiB / t, 2) for t in warm],
+               "calls": "blocking ishmem_float_sum_reduce, each returning with dest final",
+               "on_stream_back_to_back_GiBps": round(world * B / GiB / (ts / k), 2),
                "buffers": "pinned host (hipHostMalloc)" if pinned else "pageable host (malloc'd numpy)",
-               "pipeline": "H2D | reduce | D2H over 2 staging slots"}
+               "pipeline": "H2D | reduce | D2H through the staging slots (ISHMEM_STAGING_SLOTS, default 4)"}
         if pinned:
             # What bounds the leg: plain DMA copies of the same B between these pinned buffers and
             # HBM, each direction alone and both at once (the pipeline moves B each way per step).
