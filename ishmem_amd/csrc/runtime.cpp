@@ -44,6 +44,14 @@ constexpr size_t kLargeAllocBytes = (size_t) 1 << 20, kLargeAlign = (size_t) 2 <
 // slack behind copy-out; ISHMEM_STAGING_SLOTS, agreed at init (the minimum), default 4.
 constexpr int kMaxStagingSlots = 8;
 constexpr int kStagedCopyKernelDefault = 0;
+// Chunks of the staged pipeline enqueued ahead of the last one copied out.  Round 4 measured
+// (scripts/e2e_b2b.sh, e2e_big.sh, profiles/r04/host_pipeline/): with ~64 or fewer chunks queued
+// (each chunk is two copies, four event records and three stream waits) the pipeline keeps its
+// 42-45 GiB/s; with 128 queued — 4 back-to-back 1 GiB calls or one 4 GiB call in 32 MiB chunks —
+// it fell to 11-38 GiB/s, copies stalling behind the deep queues.  The window keeps the queues
+// shallow whatever the payload or the call pattern.
+constexpr int kMaxStagedWindow = 64;
+constexpr int kStagedWindowDefault = 16;
 
 thread_local std::string g_last_error;
 
@@ -219,6 +227,12 @@ struct State {
     // set_param "staged_copy_kernel"; per PE, nothing is paired).
     int staged_copy_kernel = 0;
     hipEvent_t ev_in[kMaxStagingSlots] = {}, ev_red[kMaxStagingSlots] = {}, ev_out[kMaxStagingSlots] = {};
+    // Host-side window of the staged pipeline (ISHMEM_STAGED_WINDOW chunks, 0 = off): chunk k is
+    // enqueued only once chunk k - window has been copied out, over all calls of this PE.
+    int staged_window = kStagedWindowDefault;
+    hipEvent_t win_ev[kMaxStagedWindow] = {};
+    bool win_used[kMaxStagedWindow] = {};
+    uint64_t win_seq = 0;
 
     Team teams[kMaxTeams];
     int max_blocks = kMaxBlocks;
@@ -750,6 +764,10 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
     if (!s.copy_in) {
         HIP_TRY(hipStreamCreateWithFlags(&s.copy_in, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&s.copy_out, hipStreamNonBlocking));
+        for (int i = 0; i < kMaxStagedWindow; ++i) {
+            HIP_TRY(hipEventCreateWithFlags(&s.win_ev[i], hipEventDisableTiming));
+            s.win_used[i] = false;
+        }
         for (int i = 0; i < kMaxStagingSlots; ++i) {
             HIP_TRY(hipEventCreateWithFlags(&s.ev_in[i], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s.ev_red[i], hipEventDisableTiming));
@@ -757,6 +775,8 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
         }
     }
     if (staging_acquire(s, st)) return 1;
+    // Not under capture (nothing may wait on the host then, and replays are the caller's to pace).
+    const bool throttle = s.staged_window > 0 && !capturing(st);
     HIP_TRY(hipEventRecord(s.ev_red[0], st));  // copy-ins start after the caller's prior work
     HIP_TRY(hipStreamWaitEvent(s.copy_in, s.ev_red[0], 0));
     bool used[kMaxStagingSlots] = {};
@@ -764,6 +784,8 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
         const int sl = (int) (k % (size_t) nslots);
         char *buf = s.staging + (size_t) sl * slot_bytes;
         const size_t m = std::min(chunk, n - off);
+        const int w = (int) (s.win_seq % (uint64_t) std::max(1, s.staged_window));
+        if (throttle && s.win_used[w]) HIP_TRY(hipEventSynchronize(s.win_ev[w]));  // window
         if (used[sl]) HIP_TRY(hipStreamWaitEvent(s.copy_in, s.ev_out[sl], 0));  // slot drained
         if (src_dev) {
             if (launch_copy(buf, src_dev + off * es, m * es, s.copy_in)) return 1;
@@ -788,6 +810,11 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
         }
         HIP_TRY(hipEventRecord(s.ev_out[sl], s.copy_out));
         used[sl] = true;
+        if (throttle) {
+            HIP_TRY(hipEventRecord(s.win_ev[w], s.copy_out));
+            s.win_used[w] = true;
+            ++s.win_seq;
+        }
     }
     for (int sl = 0; sl < nslots; ++sl)  // the caller's stream completes only after every copy-out
         if (used[sl]) HIP_TRY(hipStreamWaitEvent(st, s.ev_out[sl], 0));
@@ -1307,6 +1334,9 @@ int init_impl(int pe, int npes, int device, const std::string &key)
                       ~(size_t) (kHeapAlign - 1);
     s.staging_slots = (int) std::min<long long>(kMaxStagingSlots, std::max<long long>(2, env_ll("ISHMEM_STAGING_SLOTS", 4)));
     s.staged_copy_kernel = (int) (env_ll("ISHMEM_STAGED_COPY_KERNEL", kStagedCopyKernelDefault) & 3);
+    s.staged_window = (int) std::min<long long>(kMaxStagedWindow,
+                                                std::max<long long>(0, env_ll("ISHMEM_STAGED_WINDOW", kStagedWindowDefault)));
+    s.win_seq = 0;
     const size_t heap_request = env_size("ISHMEM_SYMMETRIC_SIZE", (size_t) 4 << 30);
     if (!g_env_error.empty()) {
         const std::string e = g_env_error;
@@ -1734,6 +1764,12 @@ int ishmemi_c_finalize(void)
         (void) hipStreamDestroy(s.copy_out);
         for (int i = 0; i < kMaxStagingSlots; ++i) {
             (void) hipEventDestroy(s.ev_in[i]);
+            if (i == 0)
+                for (int k = 0; k < kMaxStagedWindow; ++k) {
+                    (void) hipEventDestroy(s.win_ev[k]);
+                    s.win_ev[k] = nullptr;
+                    s.win_used[k] = false;
+                }
             (void) hipEventDestroy(s.ev_red[i]);
             (void) hipEventDestroy(s.ev_out[i]);
         }
@@ -2423,6 +2459,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     const std::string n = name ? name : "";
     if (n == "max_blocks") s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, value));
     else if (n == "staged_copy_kernel") s.staged_copy_kernel = (int) (value & 3);
+    else if (n == "staged_window") s.staged_window = (int) std::min<long long>(kMaxStagedWindow, std::max<long long>(0, value));
     else if (n == "wait_slots") set_wait_slots((int) std::min<long long>(1 << 20, std::max<long long>(1, value)));
     else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
     else if (n == "stream_order") s.stream_order = value != 0;
@@ -2446,6 +2483,7 @@ long long ishmemi_c_get_param(const char *name)
     const std::string n = name ? name : "";
     if (n == "max_blocks") return s.max_blocks;
     if (n == "staged_copy_kernel") return s.staged_copy_kernel;
+    if (n == "staged_window") return s.staged_window;
     if (n == "wait_slots") return wait_slots();
     if (n == "timeout_ms") return s.timeout_ms;
     if (n == "stream_order") return s.stream_order ? 1 : 0;

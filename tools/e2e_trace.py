@@ -34,6 +34,21 @@ def main() -> None:
             raise RuntimeError(ish.last_error())
 
     out = {}
+    if os.environ.get("E2E_BIG"):
+        # One call over a larger payload: do many chunks queued by ONE call slow down like
+        # back-to-back calls do?
+        nb = int(os.environ["E2E_BIG"]) << 30
+        bs, bd = hip.host_malloc(nb), hip.host_malloc(nb)
+        rates = []
+        for _ in range(4):
+            t0 = time.perf_counter()
+            if ish.ishmemx_float_sum_reduce_on_stream(bd, bs, nb // 4, 0, st) != 0:
+                raise RuntimeError(ish.last_error())
+            hip.stream_synchronize(st)
+            rates.append(round(nb / GiB / (time.perf_counter() - t0), 2))
+        print(json.dumps({f"single_{nb >> 30}GiB_calls": rates}), flush=True)
+        hip.host_free(bs)
+        hip.host_free(bd)
     for phase in ("warmup", "back_to_back", "synced", "back_to_back_2", "synced_2"):
         rates = []
         if phase.startswith("back_to_back"):
