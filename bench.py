@@ -650,7 +650,7 @@ def e2e_leg(ish, hip, n, B, world, rank, dist, stream, barrier, steps, pinned: b
                "calls": "blocking ishmem_float_sum_reduce, each returning with dest final",
                "on_stream_back_to_back_GiBps": round(world * B / GiB / (ts / k), 2),
                "buffers": "pinned host (hipHostMalloc)" if pinned else "pageable host (malloc'd numpy)",
-               "pipeline": "H2D | reduce | D2H through the staging slots (ISHMEM_STAGING_SLOTS, default 4)"}
+               "pipeline": "H2D | reduce | D2H through the staging slots (ISHMEM_STAGING_SLOTS, default 2 x 64 MiB)"}
         if pinned:
             # What bounds the leg: plain DMA copies of the same B between these pinned buffers and
             # HBM, each direction alone and both at once (the pipeline moves B each way per step).

@@ -39,19 +39,17 @@ constexpr size_t kHeapAlign = 256;
 // Offset of team_exchange's arrays in the host-mapped error-word allocation (after the words).
 constexpr size_t kErrExchOffset = ((kMaxTeams + 1) * sizeof(uint32_t) + 63) & ~(size_t) 63;
 constexpr size_t kLargeAllocBytes = (size_t) 1 << 20, kLargeAlign = (size_t) 2 << 20;
-// Slots of the host-memory pipeline (reduce_staged): chunk k uses slot k mod slots.  More slots
-// shorten the pipeline's fill and drain (a chunk is staging / slots bytes) and give copy-in more
-// slack behind copy-out; ISHMEM_STAGING_SLOTS, agreed at init (the minimum), default 4.
+// Slots of the host-memory pipeline (reduce_staged): chunk k uses slot k mod slots, a chunk is
+// staging / slots bytes; ISHMEM_STAGING_SLOTS, agreed at init (the minimum).  Default 2, i.e.
+// 64 MiB chunks of the 128 MiB region (round 4, scripts/e2e_b2b.sh / e2e_window.sh,
+// profiles/r04/host_pipeline/queue_depth/): with 32 MiB chunks (4 slots) single calls of 4-8 GiB
+// and back-to-back 1 GiB calls fell to 11-38 GiB/s in most runs, with 64 MiB chunks they held
+// 42.5-45.5; single synced 1 GiB calls are 42-44 either way (the copy engines do not keep both
+// directions streaming on 32 MiB transfers queued deep; a host-side window of chunks in flight,
+// tried, made it worse: 19-25 GiB/s).
 constexpr int kMaxStagingSlots = 8;
+constexpr int kStagingSlotsDefault = 2;
 constexpr int kStagedCopyKernelDefault = 0;
-// Chunks of the staged pipeline enqueued ahead of the last one copied out.  Round 4 measured
-// (scripts/e2e_b2b.sh, e2e_big.sh, profiles/r04/host_pipeline/): with ~64 or fewer chunks queued
-// (each chunk is two copies, four event records and three stream waits) the pipeline keeps its
-// 42-45 GiB/s; with 128 queued — 4 back-to-back 1 GiB calls or one 4 GiB call in 32 MiB chunks —
-// it fell to 11-38 GiB/s, copies stalling behind the deep queues.  The window keeps the queues
-// shallow whatever the payload or the call pattern.
-constexpr int kMaxStagedWindow = 64;
-constexpr int kStagedWindowDefault = 16;
 
 thread_local std::string g_last_error;
 
@@ -221,18 +219,12 @@ struct State {
     // next user waits on it, whatever stream it runs on.
     hipEvent_t staging_ev = nullptr;
     bool staging_used = false;
-    int staging_slots = 4;
+    int staging_slots = kStagingSlotsDefault;
     // Host buffers the GPU can address (pinned / registered): copy chunks in (bit 1) / out (bit 0)
     // of the staging region with the copy KERNEL instead of the DMA engines (ISHMEM_STAGED_COPY_KERNEL,
     // set_param "staged_copy_kernel"; per PE, nothing is paired).
     int staged_copy_kernel = 0;
     hipEvent_t ev_in[kMaxStagingSlots] = {}, ev_red[kMaxStagingSlots] = {}, ev_out[kMaxStagingSlots] = {};
-    // Host-side window of the staged pipeline (ISHMEM_STAGED_WINDOW chunks, 0 = off): chunk k is
-    // enqueued only once chunk k - window has been copied out, over all calls of this PE.
-    int staged_window = kStagedWindowDefault;
-    hipEvent_t win_ev[kMaxStagedWindow] = {};
-    bool win_used[kMaxStagedWindow] = {};
-    uint64_t win_seq = 0;
 
     Team teams[kMaxTeams];
     int max_blocks = kMaxBlocks;
@@ -764,10 +756,6 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
     if (!s.copy_in) {
         HIP_TRY(hipStreamCreateWithFlags(&s.copy_in, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&s.copy_out, hipStreamNonBlocking));
-        for (int i = 0; i < kMaxStagedWindow; ++i) {
-            HIP_TRY(hipEventCreateWithFlags(&s.win_ev[i], hipEventDisableTiming));
-            s.win_used[i] = false;
-        }
         for (int i = 0; i < kMaxStagingSlots; ++i) {
             HIP_TRY(hipEventCreateWithFlags(&s.ev_in[i], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&s.ev_red[i], hipEventDisableTiming));
@@ -775,8 +763,6 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
         }
     }
     if (staging_acquire(s, st)) return 1;
-    // Not under capture (nothing may wait on the host then, and replays are the caller's to pace).
-    const bool throttle = s.staged_window > 0 && !capturing(st);
     HIP_TRY(hipEventRecord(s.ev_red[0], st));  // copy-ins start after the caller's prior work
     HIP_TRY(hipStreamWaitEvent(s.copy_in, s.ev_red[0], 0));
     bool used[kMaxStagingSlots] = {};
@@ -784,8 +770,6 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
         const int sl = (int) (k % (size_t) nslots);
         char *buf = s.staging + (size_t) sl * slot_bytes;
         const size_t m = std::min(chunk, n - off);
-        const int w = (int) (s.win_seq % (uint64_t) std::max(1, s.staged_window));
-        if (throttle && s.win_used[w]) HIP_TRY(hipEventSynchronize(s.win_ev[w]));  // window
         if (used[sl]) HIP_TRY(hipStreamWaitEvent(s.copy_in, s.ev_out[sl], 0));  // slot drained
         if (src_dev) {
             if (launch_copy(buf, src_dev + off * es, m * es, s.copy_in)) return 1;
@@ -810,11 +794,6 @@ int reduce_staged_pipeline(State &s, int team, int op, int dt, void *dst, const 
         }
         HIP_TRY(hipEventRecord(s.ev_out[sl], s.copy_out));
         used[sl] = true;
-        if (throttle) {
-            HIP_TRY(hipEventRecord(s.win_ev[w], s.copy_out));
-            s.win_used[w] = true;
-            ++s.win_seq;
-        }
     }
     for (int sl = 0; sl < nslots; ++sl)  // the caller's stream completes only after every copy-out
         if (used[sl]) HIP_TRY(hipStreamWaitEvent(st, s.ev_out[sl], 0));
@@ -1332,11 +1311,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     if (s.phased_min < 0) s.phased_min = kPhasedOff;
     s.staging_bytes = (env_size("ISHMEM_STAGING_SIZE", (size_t) 128 << 20) + kHeapAlign - 1) &
                       ~(size_t) (kHeapAlign - 1);
-    s.staging_slots = (int) std::min<long long>(kMaxStagingSlots, std::max<long long>(2, env_ll("ISHMEM_STAGING_SLOTS", 4)));
+    s.staging_slots = (int) std::min<long long>(kMaxStagingSlots, std::max<long long>(2, env_ll("ISHMEM_STAGING_SLOTS", kStagingSlotsDefault)));
     s.staged_copy_kernel = (int) (env_ll("ISHMEM_STAGED_COPY_KERNEL", kStagedCopyKernelDefault) & 3);
-    s.staged_window = (int) std::min<long long>(kMaxStagedWindow,
-                                                std::max<long long>(0, env_ll("ISHMEM_STAGED_WINDOW", kStagedWindowDefault)));
-    s.win_seq = 0;
     const size_t heap_request = env_size("ISHMEM_SYMMETRIC_SIZE", (size_t) 4 << 30);
     if (!g_env_error.empty()) {
         const std::string e = g_env_error;
@@ -1764,12 +1740,6 @@ int ishmemi_c_finalize(void)
         (void) hipStreamDestroy(s.copy_out);
         for (int i = 0; i < kMaxStagingSlots; ++i) {
             (void) hipEventDestroy(s.ev_in[i]);
-            if (i == 0)
-                for (int k = 0; k < kMaxStagedWindow; ++k) {
-                    (void) hipEventDestroy(s.win_ev[k]);
-                    s.win_ev[k] = nullptr;
-                    s.win_used[k] = false;
-                }
             (void) hipEventDestroy(s.ev_red[i]);
             (void) hipEventDestroy(s.ev_out[i]);
         }
@@ -2459,7 +2429,6 @@ int ishmemi_c_set_param(const char *name, long long value)
     const std::string n = name ? name : "";
     if (n == "max_blocks") s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, value));
     else if (n == "staged_copy_kernel") s.staged_copy_kernel = (int) (value & 3);
-    else if (n == "staged_window") s.staged_window = (int) std::min<long long>(kMaxStagedWindow, std::max<long long>(0, value));
     else if (n == "wait_slots") set_wait_slots((int) std::min<long long>(1 << 20, std::max<long long>(1, value)));
     else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
     else if (n == "stream_order") s.stream_order = value != 0;
@@ -2483,7 +2452,6 @@ long long ishmemi_c_get_param(const char *name)
     const std::string n = name ? name : "";
     if (n == "max_blocks") return s.max_blocks;
     if (n == "staged_copy_kernel") return s.staged_copy_kernel;
-    if (n == "staged_window") return s.staged_window;
     if (n == "wait_slots") return wait_slots();
     if (n == "timeout_ms") return s.timeout_ms;
     if (n == "stream_order") return s.stream_order ? 1 : 0;
