@@ -164,8 +164,9 @@ struct PeRecord {
     int32_t flags_kind_requested;  // ISHMEM_FLAGS_KIND (tests): where this PE's ladder started
     char pci_bus[32];  // identifies the physical GPU across processes
     uint64_t heap_size;
-    // Launch-shape parameters: the multi-PE kernels pair workgroup b with workgroup b of every
-    // peer and choose the LL path per call, so every PE must use the same values.
+    // Path-choosing parameters (LL / two-member one-shot / phased, staging chunks): every PE must
+    // take the same path per call, so init agrees on them.  max_blocks travels for diagnostics
+    // only: the kernels grab work, so the grid cap is per PE.
     int64_t max_blocks, ll_max_bytes, oneshot_p2, phased_min;
     uint64_t staging_bytes;
     int64_t staging_slots;

@@ -166,7 +166,7 @@ def count_wrong(hip, ptr: int, op: str, npd, p: int, lo: int, m: int, chunk: int
 def _base(pe: int, n: int) -> np.ndarray:
     # Deterministic full-range int32 words per PE (xorshift-multiply hash of the index).
     i = np.arange(n, dtype=np.uint64)
-    x = (i + np.uint64(0x9E3779B97F4A7C15) * np.uint64(pe + 1)) & np.uint64(0xFFFFFFFFFFFFFFFF)
+    x = i + np.uint64((0x9E3779B97F4A7C15 * (pe + 1)) & 0xFFFFFFFFFFFFFFFF)  # wraps mod 2^64
     x ^= x >> np.uint64(29)
     x = (x * np.uint64(0xBF58476D1CE4E5B9)) & np.uint64(0xFFFFFFFFFFFFFFFF)
     x ^= x >> np.uint64(32)
