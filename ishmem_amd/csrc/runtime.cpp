@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <errno.h>
 #include <sys/prctl.h>
 #include <unistd.h>
 
@@ -129,10 +130,27 @@ size_t env_size(const char *name, size_t dflt)
     return (size_t) v;
 }
 
+// Integers from the environment: decimal, surrounding blanks allowed.  A malformed ISHMEM_*
+// value fails init with the variable named, like a malformed byte count ("4x", "sixteen" and
+// out-of-range values used to parse as a prefix or wrap); other variables (HIP's) fall back to
+// the default.
 long long env_ll(const char *name, long long dflt)
 {
     const char *s = getenv(name);
-    return (s && *s) ? atoll(s) : dflt;
+    if (!s || !*s) return dflt;
+    const char *b = s;
+    while (*b == ' ' || *b == '\t') ++b;
+    char *end = nullptr;
+    errno = 0;
+    const long long v = strtoll(b, &end, 10);
+    const char *e = end;
+    while (*e == ' ' || *e == '\t') ++e;
+    if (end == b || *e || errno == ERANGE) {
+        if (strncmp(name, "ISHMEM_", 7) == 0 && g_env_error.empty())
+            g_env_error = std::string(name) + "='" + s + "' is not an integer";
+        return dflt;
+    }
+    return v;
 }
 
 struct Team {
@@ -225,6 +243,7 @@ struct State {
     // of the staging region with the copy KERNEL instead of the DMA engines (ISHMEM_STAGED_COPY_KERNEL,
     // set_param "staged_copy_kernel"; per PE, nothing is paired).
     int staged_copy_kernel = 0;
+    bool test_flags_unavailable = false;  // ISHMEM_TEST_FLAGS_UNAVAILABLE (alloc_flags)
     hipEvent_t ev_in[kMaxStagingSlots] = {}, ev_red[kMaxStagingSlots] = {}, ev_out[kMaxStagingSlots] = {};
 
     Team teams[kMaxTeams];
@@ -1258,7 +1277,7 @@ int alloc_flags(State &s, int kind, bool exportable, hipIpcMemHandle_t *h)
     const size_t bytes = kFlagAllocBytes;
     // Test hook: behave as if uncached / fine-grained VRAM could not be allocated (the refusal of
     // coarse-grained flags across devices is tested with it on a one-GPU box).
-    if (env_ll("ISHMEM_TEST_FLAGS_UNAVAILABLE", 0) != 0) kind = kFlagsCoarse;
+    if (s.test_flags_unavailable) kind = kFlagsCoarse;
     for (int k = kind; k < kFlagKinds; ++k) {
         uint32_t *f = nullptr;
         hipError_t e = k == kFlagsUncached ? hipExtMallocWithFlags((void **) &f, bytes, hipDeviceMallocUncached)
@@ -1315,6 +1334,10 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.staging_slots = (int) std::min<long long>(kMaxStagingSlots, std::max<long long>(2, env_ll("ISHMEM_STAGING_SLOTS", kStagingSlotsDefault)));
     s.staged_copy_kernel = (int) (env_ll("ISHMEM_STAGED_COPY_KERNEL", kStagedCopyKernelDefault) & 3);
     const size_t heap_request = env_size("ISHMEM_SYMMETRIC_SIZE", (size_t) 4 << 30);
+    // ISHMEM_FLAGS_KIND (tests): start the flag-memory ladder at FlagMem 1 or 2 instead of uncached VRAM.
+    const int first_kind = (int) std::min<long long>(kFlagsCoarse, std::max<long long>(0, env_ll("ISHMEM_FLAGS_KIND", 0)));
+    s.test_flags_unavailable = env_ll("ISHMEM_TEST_FLAGS_UNAVAILABLE", 0) != 0;
+    const bool ep_uncached = env_ll("ISHMEM_EP_UNCACHED", 0) != 0;
     if (!g_env_error.empty()) {
         const std::string e = g_env_error;
         g_env_error.clear();
@@ -1336,9 +1359,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.free_list[0] = s.heap_size;
 
     // Barrier flags (written by peers over xGMI): the best memory kind that can also be exported.
-    // ISHMEM_FLAGS_KIND (tests): start the ladder at FlagMem 1 or 2 instead of uncached VRAM.
     hipIpcMemHandle_t flags_handle{};
-    const int first_kind = (int) std::min<long long>(kFlagsCoarse, std::max<long long>(0, env_ll("ISHMEM_FLAGS_KIND", 0)));
     if (alloc_flags(s, first_kind, npes > 1, &flags_handle)) return 1;
     HIP_TRY(hipHostMalloc((void **) &s.err_host, kErrExchOffset + 2 * kMaxPes * sizeof(uint64_t),
                           hipHostMallocMapped | hipHostMallocCoherent));
@@ -1516,7 +1537,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     // counters) and system-scope loads/stores (the epoch), which do not depend on the memory
     // type; ordinary device memory (ISHMEM_EP_UNCACHED=1: fine-grained uncached, for comparison).
     const size_t ep_bytes = (size_t) kEpTeamWords * kMaxTeams * sizeof(uint32_t);
-    if (env_ll("ISHMEM_EP_UNCACHED", 0) == 0 ||
+    if (!ep_uncached ||
         hipExtMallocWithFlags((void **) &s.kern_ep, ep_bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void) hipGetLastError();
         HIP_TRY(hipMalloc((void **) &s.kern_ep, ep_bytes));

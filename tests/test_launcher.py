@@ -146,11 +146,16 @@ print("rc=%d|%s" % (rc, L.ishmemi_c_last_error().decode()))
     ("ISHMEM_LL_MAX_BYTES", "64KQ", True), ("ISHMEM_SYMMETRIC_SIZE", "-4G", True),
     ("ISHMEM_STAGING_SIZE", "nan", True), ("ISHMEM_PHASED_MIN_BYTES", "1e30", False),
     ("ISHMEM_PHASED_MIN_BYTES", " 16MiB ", False), ("ISHMEM_LL_MAX_BYTES", "64kb", False),
-    ("ISHMEM_SYMMETRIC_SIZE", "2T", False), ("ISHMEM_PHASED_MIN_BYTES", "-1", False)])
+    ("ISHMEM_SYMMETRIC_SIZE", "2T", False), ("ISHMEM_PHASED_MIN_BYTES", "-1", False),
+    # integer variables: the same rule (a prefix such as "16x" -> 16 used to pass silently)
+    ("ISHMEM_WAIT_SLOTS", "16x", True), ("ISHMEM_STAGING_SLOTS", "four", True),
+    ("ISHMEM_TIMEOUT_MS", "99999999999999999999", True), ("ISHMEM_FLAGS_KIND", "1.5", True),
+    ("ISHMEM_MAX_BLOCKS", " 256 ", False), ("ISHMEM_TIMEOUT_MS", "-5", False)])
 def test_byte_count_variables_parse_strictly(name, value, bad):
     """byte-count variables choose kernel paths every PE must agree on, so a typo
     fails init with the variable named instead of parsing as something else; values past LLONG_MAX
-    clamp.  Checked before any GPU call (here the init then fails for want of a device, or not at
+    clamp.  Integer ISHMEM_* variables (grid caps, slots, timeouts, test hooks) are held to the same
+    rule.  Checked before any GPU call (here the init then fails for want of a device, or not at
     all on a GPU box — either way not on the variable)."""
     out = subprocess.run([sys.executable, "-c", ENV_PROBE, str(ROOT)], env=clean_env(**{name: value}),
                          capture_output=True, text=True, timeout=120)
