@@ -291,6 +291,8 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
               footprint"; 16 = 64 workgroups is the default) — whether that grid fills the links;
       phased - 2 / 4 / 8 / 16 / 64 MiB and the payload on the phased path (one-shot grids
                between barriers) and on the persistent kernel (the phased threshold, 4 MiB);
+      phased_peer_nt - 64 MiB and the payload on the phased path with nontemporal peer loads
+               (the collectives issue sc0 sc1 ones; the tripwire_peer_nt leg checks coherence);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
       ll    - 4 / 16 / 64 KiB with the one-hop granule path on (default) and off."""
 
@@ -334,6 +336,9 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
         if nb <= B:
             run("phased", "phased_min_bytes", 0, nb, 5 if nb == B else 20)
             run("persistent", "phased_min_bytes", -1, nb, 5 if nb == B else 20)
+    for nb in sorted({64 << 20, B}):
+        if nb <= B:  # the phased grids' peer loads nontemporal instead of sc0 sc1 (measurement only)
+            run("phased_peer_nt", "phased_peer_nt", 1, nb, 5 if nb == B else 20, also={"phased_min_bytes": 0})
     if world == 2:
         run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
         run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)
@@ -879,6 +884,23 @@ def main() -> int:
             extra["tripwire"] = tw
         except Exception as ex:
             extra["tripwire"] = {"error": str(ex), "checked": False}
+        if healthy() and not args.no_tuning:
+            # The same chained producer -> reduce check with the phased grids' peer loads
+            # nontemporal (measurement mode, phased path forced): does the kernel-boundary acquire
+            # alone keep peers' bytes fresh across devices?  Reported, never fatal.
+            old_nt, old_min = ish.get_param("phased_peer_nt"), ish.get_param("phased_min_bytes")
+            try:
+                ish.set_param("phased_peer_nt", 1)
+                ish.set_param("phased_min_bytes", 0)
+                tw = selfcheck.chain_tripwire(ish, hip, rank, world, nmax=16 << 20, iters=8, stream=stream)
+                bad = max_over_ranks(dist, [float(sum(tw["mismatches"])), float(not tw["checked"])])
+                extra["tripwire_peer_nt"] = {"checked": bad[0] == 0 and bad[1] == 0,
+                                             "mismatches_all_ranks": int(bad[0]), "iters": tw["iters"]}
+            except Exception as ex:
+                extra["tripwire_peer_nt"] = {"error": str(ex), "checked": False}
+            finally:
+                ish.set_param("phased_peer_nt", old_nt)
+                ish.set_param("phased_min_bytes", old_min)
 
     if world > 1 and healthy() and not args.no_sweep:
         log("config-5 sweep")

@@ -171,6 +171,10 @@ struct PhaseArgs {
     uint64_t items_per_chunk;     // the reduce-scatter partition (a multiple of 64 items)
     uint32_t elem;                // element bytes (the all-gather copies head / tail bytes)
     int p, me;
+    // Measurement only (set_param "phased_peer_nt", default 0): load peers' bytes with nontemporal
+    // loads instead of system-coherent (sc0 sc1) ones, leaning on the kernel-boundary acquire for
+    // visibility.  For the N > 1 bench's A/B over xGMI (speed, and the tripwire for coherence).
+    int peer_nt;
 };
 hipError_t launch_rs_phase(int op, int dt, const PhaseArgs &a, hipStream_t s);
 hipError_t launch_ag_phase(const PhaseArgs &a, hipStream_t s);

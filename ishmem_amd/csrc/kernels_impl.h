@@ -965,7 +965,7 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
 // here) starts after the middle barrier.  The price is two more launches and two more barrier
 // round trips than the persistent kernel (~10 us), so it is used for large payloads only.
 // ---------------------------------------------------------------------------------------------
-template <typename T, int OP, int P, int R>
+template <typename T, int OP, int P, bool NT, int R>
 __device__ __forceinline__ void rs_phase_item(const PhaseArgs &a, uint64_t wb, bool valid)
 {
     using Item = Vec<T>;
@@ -975,7 +975,7 @@ __device__ __forceinline__ void rs_phase_item(const PhaseArgs &a, uint64_t wb, b
     for (int k = 0; k < P; ++k) {
         const int j = (R + k) % P;
         if (!valid) continue;
-        if (j == a.me) x[k] = nt_load((const Item *) (a.src[j] + wb + off));
+        if (NT || j == a.me) x[k] = nt_load((const Item *) (a.src[j] + wb + off));
         else x[k] = cload<Item>(make_rsrc(uniform_ptr(a.src[j] + wb)), off);
     }
     Item acc = x[(P - R) % P];  // member 0
@@ -984,14 +984,14 @@ __device__ __forceinline__ void rs_phase_item(const PhaseArgs &a, uint64_t wb, b
     if (valid) wt_store(make_rsrc(uniform_ptr(a.dst + wb)), off, acc);
 }
 
-template <typename T, int OP, int P, int R = 0>
+template <typename T, int OP, int P, bool NT, int R = 0>
 __device__ __forceinline__ void rs_phase_dispatch(const PhaseArgs &a, int rot, uint64_t wb, bool valid)
 {
     if constexpr (R == P - 1) {
-        rs_phase_item<T, OP, P, R>(a, wb, valid);
+        rs_phase_item<T, OP, P, NT, R>(a, wb, valid);
     } else {
-        if (rot == R) rs_phase_item<T, OP, P, R>(a, wb, valid);
-        else rs_phase_dispatch<T, OP, P, R + 1>(a, rot, wb, valid);
+        if (rot == R) rs_phase_item<T, OP, P, NT, R>(a, wb, valid);
+        else rs_phase_dispatch<T, OP, P, NT, R + 1>(a, rot, wb, valid);
     }
 }
 
@@ -1005,7 +1005,7 @@ __device__ __forceinline__ void rs_phase_item_any(const PhaseArgs &a, uint64_t w
     Item acc;
     for (int j = 0; j < a.p; ++j) {
         Item x;
-        if (j == a.me) x = nt_load((const Item *) (a.src[j] + wb + off));
+        if (j == a.me || a.peer_nt) x = nt_load((const Item *) (a.src[j] + wb + off));
         else x = cload<Item>(make_rsrc(uniform_ptr(a.src[j] + wb)), off);
         acc = j == 0 ? x : op1<T, OP>(acc, x);
     }
@@ -1020,12 +1020,16 @@ __global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
     const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
     const uint64_t head_bytes = a.head * sizeof(T);
     const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
-    for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kFaninBlock; i0 < ce; i0 += stride) {
-        const bool valid = i0 + threadIdx.x < ce;
-        const uint64_t wb = head_bytes + i0 * 16;
-        if constexpr (P > 0) rs_phase_dispatch<T, OP, P>(a, (int) ((i0 / kFaninBlock) % P), wb, valid);
-        else rs_phase_item_any<T, OP>(a, wb, valid);
-    }
+    auto body = [&](auto nt) {
+        for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kFaninBlock; i0 < ce; i0 += stride) {
+            const bool valid = i0 + threadIdx.x < ce;
+            const uint64_t wb = head_bytes + i0 * 16;
+            if constexpr (P > 0) rs_phase_dispatch<T, OP, P, decltype(nt)::value>(a, (int) ((i0 / kFaninBlock) % P), wb, valid);
+            else rs_phase_item_any<T, OP>(a, wb, valid);
+        }
+    };
+    if (a.peer_nt) body(std::true_type{});
+    else body(std::false_type{});
     // Unaligned head (member 0's) and tail (member p-1's), element-wise, by workgroup 0;
     // descriptors based at the region (offsets < 16 B).
     if (blockIdx.x == 0) {
@@ -1069,7 +1073,8 @@ __global__ __launch_bounds__(kFaninBlock) void ag_phase_kernel(PhaseArgs a)
         const uint64_t i0 = js + (w / peers) * kFaninBlock;
         if (i0 + threadIdx.x < je) {
             const uint64_t wb = head_bytes + i0 * 16;
-            const u32x4 x = cload<u32x4>(make_rsrc(uniform_ptr(a.dstp[j] + wb)), off);
+            const u32x4 x = a.peer_nt ? nt_load((const u32x4 *) (a.dstp[j] + wb + off))
+                                      : cload<u32x4>(make_rsrc(uniform_ptr(a.dstp[j] + wb)), off);
             wt_store(make_rsrc(uniform_ptr(a.dst + wb)), off, x);
         }
     }

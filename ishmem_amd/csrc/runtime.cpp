@@ -244,6 +244,9 @@ struct State {
     // set_param "staged_copy_kernel"; per PE, nothing is paired).
     int staged_copy_kernel = 0;
     bool test_flags_unavailable = false;  // ISHMEM_TEST_FLAGS_UNAVAILABLE (alloc_flags)
+    // Measurement only (set_param "phased_peer_nt"): the phased grids load peers' bytes
+    // nontemporal instead of sc0 sc1 (kernels.h PhaseArgs::peer_nt).  Must be set alike on every PE.
+    int phased_peer_nt = 0;
     hipEvent_t ev_in[kMaxStagingSlots] = {}, ev_red[kMaxStagingSlots] = {}, ev_out[kMaxStagingSlots] = {};
 
     Team teams[kMaxTeams];
@@ -636,6 +639,7 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         ph.elem = (uint32_t) es;
         ph.p = t.size;
         ph.me = t.my_idx;
+        ph.peer_nt = s.phased_peer_nt;
         const bool ev = s.phase_events && !capturing(st);
         auto mark = [&](int k) -> int {
             if (ev) HIP_TRY(hipEventRecord(s.phase_ev[k], st));
@@ -1338,6 +1342,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     const int first_kind = (int) std::min<long long>(kFlagsCoarse, std::max<long long>(0, env_ll("ISHMEM_FLAGS_KIND", 0)));
     s.test_flags_unavailable = env_ll("ISHMEM_TEST_FLAGS_UNAVAILABLE", 0) != 0;
     const bool ep_uncached = env_ll("ISHMEM_EP_UNCACHED", 0) != 0;
+    s.phased_peer_nt = env_ll("ISHMEM_PHASED_PEER_NT", 0) != 0;
     if (!g_env_error.empty()) {
         const std::string e = g_env_error;
         g_env_error.clear();
@@ -2458,6 +2463,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "phased_min_bytes") s.phased_min = value < 0 ? kPhasedOff : value;
     else if (n == "ll_max_bytes") s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes, std::max<long long>(0, value));
     else if (n == "debug") s.debug = (int) value;
+    else if (n == "phased_peer_nt") s.phased_peer_nt = value != 0;
     else if (n == "trace_buffer") s.trace = (uint64_t *) (uintptr_t) value;
     else if (n == "phase_events") {
         if (value && !s.phase_ev[0])
@@ -2481,6 +2487,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "phased_min_bytes") return s.phased_min == kPhasedOff ? -1 : s.phased_min;
     if (n == "ll_max_bytes") return s.ll_max_bytes;
     if (n == "debug") return s.debug;
+    if (n == "phased_peer_nt") return s.phased_peer_nt;
     if (n == "flags_fine_grained") return s.flags_kind != kFlagsCoarse ? 1 : 0;
     if (n == "flags_kind") return s.flags_kind;
     if (n == "staging_bytes") return (long long) s.staging_bytes;

@@ -166,6 +166,18 @@ def test_phased_reduce_scatter_allgather_path(npes):
             timeout=400)
 
 
+@pytest.mark.parametrize("npes", [2, 4])
+def test_phased_path_with_nontemporal_peer_loads(npes):
+    # The measurement-only mode the N > 1 bench times over xGMI (ISHMEM_PHASED_PEER_NT /
+    # set_param "phased_peer_nt": the phased grids load peers' bytes nontemporal instead of sc0 sc1,
+    # relying on the kernel-boundary acquire).  On one GPU it must give the same bytes; whether it
+    # stays coherent across devices is what the bench's tripwire_peer_nt leg records on the node.
+    run_pes(npes, ["golden", "inplace", "offsets", "large", "tripwire"],
+            env={"ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_ONESHOT_P2_MAX_BYTES": 0,
+                 "ISHMEM_PHASED_PEER_NT": 1, "ISHMEM_MAX_BLOCKS": 64},
+            timeout=400)
+
+
 @pytest.mark.parametrize("npes,scenarios", [(4, ["team", "stream", "streams", "staged"]), (6, ["teams2"])])
 def test_phased_paths_on_teams_streams_and_staged_buffers(npes, scenarios):
     # The phased paths forced, on strided / nested / 2-D teams, the reference's negative-stride,
