@@ -44,6 +44,7 @@ namespace {
 
 // sc0|sc1 cache policy on gfx950 buffer instructions = system-coherent access.
 constexpr int kSysCoherent = 17;
+constexpr int kNonTemporal = 2;  // buffer aux bits: nt
 constexpr uint64_t kTile = (uint64_t) kBlock * kUnroll;  // items per tile
 #ifndef ISHMEMI_AR_OCC
 #define ISHMEMI_AR_OCC 4  // multi-PE kernel: workgroups per CU (see allreduce_kernel)
@@ -916,6 +917,18 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
         Item acc;
         if constexpr (NS == 1) {
             acc = nt_load((const Item *) (a.src[0] + off));
+        } else if constexpr (NS == 2 && VEC) {
+            // Buffer loads based at the workgroup's first item (scalar base + 32-bit lane offset):
+            // a + b 0.471-0.472 ms against 0.484-0.485 ms with global nt loads, 1 GiB, interleaved
+            // A B x3 (profiles/r04/fanin_loads/); the copy (NS = 1) keeps global loads, which were
+            // 0.7 % faster there.
+            const uint64_t wo = off - (uint64_t) threadIdx.x * IB;
+            const uint32_t lo = (uint32_t) (threadIdx.x * IB);
+            const Item x0 = __builtin_bit_cast(Item, __builtin_amdgcn_raw_buffer_load_b128(
+                make_rsrc(uniform_ptr(a.src[0] + wo)), lo, 0, kNonTemporal));
+            const Item x1 = __builtin_bit_cast(Item, __builtin_amdgcn_raw_buffer_load_b128(
+                make_rsrc(uniform_ptr(a.src[1] + wo)), lo, 0, kNonTemporal));
+            acc = op1<T, OP>(x0, x1);
         } else if constexpr (NS == 2) {
             const Item x0 = nt_load((const Item *) (a.src[0] + off));
             const Item x1 = nt_load((const Item *) (a.src[1] + off));

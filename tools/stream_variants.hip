@@ -373,6 +373,16 @@ int main(int argc, char **argv)
         CK(hipMalloc(&a, bytes));
         CK(hipMalloc(&b, bytes));
         CK(hipMalloc(&d, bytes));
+    } else if (layout.rfind("dskew:", 0) == 0) {
+        // Round 4: operands packed in one heap, each next operand `gap` bytes past the end of the
+        // previous one (the library's 2 MiB-aligned large allocations have gap 0): does moving
+        // dest off the source's DRAM channel / bank phase change the copy's rate?
+        const long gap = atol(layout.c_str() + 6);
+        char *h;
+        CK(hipMalloc(&h, 4l << 30));
+        a = (f4 *) (h + (128l << 20));
+        d = (f4 *) ((char *) a + bytes + gap);
+        b = (f4 *) ((char *) d + bytes + gap);
     } else {
         // One heap like the library's symmetric heap: operands at `skew` bytes past 128 MiB and
         // packed back to back (heap = 256-B aligned first fit after the staging region).
@@ -454,6 +464,10 @@ int main(int argc, char **argv)
         vs.push_back({"aux ns2 bs64 ld nt / st sc0sc1 (product a+b)", OA<2, 64, 2, 17>, 0, 2});
         vs.push_back({"  a+b + 8 KiB LDS", OAL<2, 64, 2, 17, 8192>, 0, 2});
         vs.push_back({"  a+b + 16 KiB LDS", OAL<2, 64, 2, 17, 16384>, 0, 2});
+    }
+    if (set == "prod") {  // round 4: the product shapes only (layout A/B)
+        vs.push_back({"aux ns1 bs64 ld nt / st sc0sc1 (product copy)", OA<1, 64, 2, 17>, 0, 1});
+        vs.push_back({"aux ns2 bs64 ld nt / st sc0sc1 (product a+b)", OA<2, 64, 2, 17>, 0, 2});
     }
     if (set == "r3") {  // round 3: store acknowledgements on the persistent kernel's critical path
         vs.push_back({"aux ns2 bs64 ld nt / st sc0sc1 (product a+b)", OA<2, 64, 2, 17>, 0, 2});
