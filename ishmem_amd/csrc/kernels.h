@@ -158,6 +158,12 @@ struct FaninArgs {
     char *dst;
     uint64_t head, nitems, tail;
     int nsrc;
+    // Realigned body (fanin_realign_kernel, 1 or 2 sources whose addresses differ from dst's mod
+    // 16): head = elements until dst is 16-B aligned; shift[j] = source j's byte offset from the
+    // 16-B grid at that point; total = payload bytes (bounds of the sources' aligned loads).
+    int realign;
+    uint32_t shift[kMaxFanin];
+    uint64_t total;
 };
 
 // Phased reduce-scatter / all-gather of large payloads (p > 1, 16-B vector body): two one-shot

@@ -965,6 +965,80 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
 }
 
 // ---------------------------------------------------------------------------------------------
+// Realigned fan-in: 1 or 2 sources whose addresses differ from dst's mod 16, every operand
+// element-aligned (runtime.cpp plan_realign).  The element-granular path moved such operands one
+// element per lane — a 1-PE reduce (a byte copy) at 0.6 TB/s, a + b at 3.4 TB/s on 256 MiB
+// (tools/misaligned_probe.py).  Here dst is peeled to the 16-B grid (head elements, workgroup 0)
+// and every lane loads the ALIGNED 16-B vector of each source at its item, takes its neighbour
+// lane's vector with a cross-lane shuffle (lane 63 loads the next vector itself), and funnel-shifts
+// the pair by the source's byte shift (uniform: v_alignbyte on word pairs picked by a scalar
+// switch) — full-width loads and stores, HBM traffic of the aligned kernel.  The aligned loads
+// reach at most up to the source's end rounded up to 16 B (the same 16-B block, so the same page);
+// the descriptor's bound there returns zeros for lanes past the body.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_n(const char *uniform_base, uint64_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(uniform_base), (short) 0,
+                                             (int) (bytes < 0x7FFFFFFFull ? bytes : 0x7FFFFFFFull), 0x00020000);
+}
+
+// Bytes k .. k + 15 of the 32-byte concatenation A | B (k uniform, 0 <= k < 16).
+__device__ __forceinline__ u32x4 funnel16(const u32x4 &A, const u32x4 &B, uint32_t k)
+{
+    const uint32_t r = k & 3;
+    auto al = [r](uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbyte(hi, lo, r); };
+    switch (k >> 2) {
+        case 0: return u32x4{al(A.y, A.x), al(A.z, A.y), al(A.w, A.z), al(B.x, A.w)};
+        case 1: return u32x4{al(A.z, A.y), al(A.w, A.z), al(B.x, A.w), al(B.y, B.x)};
+        case 2: return u32x4{al(A.w, A.z), al(B.x, A.w), al(B.y, B.x), al(B.z, B.y)};
+        default: return u32x4{al(B.x, A.w), al(B.y, B.x), al(B.z, B.y), al(B.w, B.z)};
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ Vec<T> realigned_load(const FaninArgs &a, int j, uint64_t wo, uint32_t tid)
+{
+    const uint32_t k = a.shift[j];
+    const uint64_t start = wo - k;  // 16-B aligned in memory (dst + wo is, src + wo has residue k)
+    const char *sb = uniform_ptr(a.src[j] + start);
+    const uint64_t end_al = (((uint64_t) (uintptr_t) a.src[j] + a.total + 15) & ~15ull) - (uint64_t) (uintptr_t) sb;
+    const __amdgpu_buffer_rsrc_t r = make_rsrc_n(sb, end_al);
+    const u32x4 A = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, kNonTemporal);
+    u32x4 B;
+    B.x = __shfl_down(A.x, 1u);
+    B.y = __shfl_down(A.y, 1u);
+    B.z = __shfl_down(A.z, 1u);
+    B.w = __shfl_down(A.w, 1u);
+    if (tid == kFaninBlock - 1) B = __builtin_amdgcn_raw_buffer_load_b128(r, kFaninBlock * 16u, 0, kNonTemporal);
+    return __builtin_bit_cast(Vec<T>, funnel16(A, B, k));
+}
+
+template <typename T, int OP, int NS>
+__global__ __launch_bounds__(kFaninBlock) void fanin_realign_kernel(FaninArgs a)
+{
+    static_assert(NS == 1 || NS == 2, "realigned fan-in: 1 or 2 sources");
+    const uint32_t tid = threadIdx.x;
+    const uint64_t hb = a.head * sizeof(T);
+    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
+    for (uint64_t i0 = (uint64_t) blockIdx.x * kFaninBlock; i0 < a.nitems; i0 += stride) {
+        const uint64_t wo = hb + i0 * 16;  // bytes from element 0 to this workgroup's first item
+        Vec<T> acc = realigned_load<T>(a, 0, wo, tid);
+        if constexpr (NS == 2) acc = op1<T, OP>(acc, realigned_load<T>(a, 1, wo, tid));
+        if (i0 + tid < a.nitems) wt_store(make_rsrc(uniform_ptr(a.dst + wo)), tid * 16u, acc);
+    }
+    if (blockIdx.x == 0) {  // head elements (dst not yet on the 16-B grid) and tail elements
+        const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
+        for (int pass = 0; pass < 2; ++pass) {
+            if ((uint64_t) tid >= (pass == 0 ? a.head : a.tail)) continue;
+            const uint64_t e = pass == 0 ? (uint64_t) tid : tail_off + tid;
+            T acc = ((const T *) a.src[0])[e];
+            if constexpr (NS == 2) acc = op1<T, OP>(acc, ((const T *) a.src[1])[e]);
+            ((T *) a.dst)[e] = acc;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Phased reduce-scatter + all-gather for large payloads (runtime.cpp reduce_heap, p > 1, 16-B
 // vector body, payload >= ISHMEM_PHASED_MIN_BYTES):
 //   team_sync_kernel - every member's source is final;
@@ -1339,6 +1413,12 @@ void fi_ns(const FaninArgs &a, int grid, hipStream_t s)
 template <typename T, int OP>
 hipError_t fi_t(bool vec, const FaninArgs &a, int grid, hipStream_t s)
 {
+    if (a.realign) {
+        if (a.nsrc == 1) hipLaunchKernelGGL((fanin_realign_kernel<T, OP, 1>), dim3(grid), dim3(kFaninBlock), 0, s, a);
+        else if (a.nsrc == 2) hipLaunchKernelGGL((fanin_realign_kernel<T, OP, 2>), dim3(grid), dim3(kFaninBlock), 0, s, a);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     if (vec) fi_ns<T, OP, true>(a, grid, s);
     else fi_ns<T, OP, false>(a, grid, s);
     return hipGetLastError();

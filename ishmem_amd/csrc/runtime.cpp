@@ -483,6 +483,34 @@ Kind classify(const State &s, const void *p)
     return Kind::Host;
 }
 
+// Fan-in operands whose addresses differ mod 16 (no common vector body): with 1 or 2 sources and
+// every operand element-aligned, the realigned kernel (kernels_impl.h fanin_realign_kernel) runs
+// the body at full vector width; otherwise the element-granular path.  Every PE computes the same
+// plan for the same addresses, and the fan-in never touches peers, so nothing is paired.
+constexpr size_t kRealignMinBytes = 1024;
+
+void plan_fanin(FaninArgs &f, Plan &pl, const void *dst, const void *const *srcs, int nsrc, size_t n, size_t es)
+{
+    pl = make_plan(dst, srcs, nsrc, n, es, 1, 0, kFaninMaxGrid);
+    f.head = pl.head;
+    f.nitems = pl.nitems;
+    f.tail = pl.tail;
+    f.realign = 0;
+    const uintptr_t d = (uintptr_t) dst;
+    bool ok = !pl.vec && nsrc >= 1 && nsrc <= 2 && n * es >= kRealignMinBytes && d % es == 0;
+    for (int j = 0; ok && j < nsrc; ++j) ok = (uintptr_t) srcs[j] % es == 0;
+    if (!ok) return;
+    const uint64_t h = std::min<uint64_t>(n, ((16 - d % 16) % 16) / es);
+    f.head = h;
+    f.nitems = (n - h) * es / 16;
+    f.tail = n - h - f.nitems * (16 / es);
+    for (int j = 0; j < nsrc; ++j) f.shift[j] = (uint32_t) (((uintptr_t) srcs[j] + h * es) % 16);
+    f.total = n * es;
+    f.realign = 1;
+    pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((f.nitems + kFaninBlock - 1) / kFaninBlock,
+                                                             (uint64_t) kFaninMaxGrid));
+}
+
 int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)
 {
     if (bytes == 0 || dst == src) return 0;
@@ -491,10 +519,8 @@ int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)
     f.dst = (char *) dst;
     f.nsrc = 1;
     const void *srcs[1] = {src};
-    Plan pl = make_plan(dst, srcs, 1, bytes, 1, 1, 0, kFaninMaxGrid);
-    f.head = pl.head;
-    f.nitems = pl.nitems;
-    f.tail = pl.tail;
+    Plan pl;
+    plan_fanin(f, pl, dst, srcs, 1, bytes, 1);
     HIP_TRY(launch_fanin(ISHMEMI_OP_OR, ISHMEMI_DT_UINT8, pl.vec, f, pl.grid, st));
     return 0;
 }
@@ -2205,10 +2231,8 @@ int ishmemi_c_combine(int op, int dtype, void *dst, const void *const *srcs, int
     }
     f.dst = (char *) dst;
     f.nsrc = nsrc;
-    Plan pl = make_plan(dst, srcs, nsrc, n, dtype_size(dtype), 1, 0, kFaninMaxGrid);
-    f.head = pl.head;
-    f.nitems = pl.nitems;
-    f.tail = pl.tail;
+    Plan pl;
+    plan_fanin(f, pl, dst, srcs, nsrc, n, dtype_size(dtype));
     HIP_TRY(launch_fanin(op, dtype, pl.vec, f, pl.grid, (hipStream_t) stream));
     return 0;
 }

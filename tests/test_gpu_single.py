@@ -69,6 +69,68 @@ def test_combine_misaligned_operands(ish, dt):
         hip.free(p)
 
 
+@pytest.mark.parametrize("dt", [0, 2, 3, 8, 9])
+def test_combine_realigned_operands(ish, dt):
+    # Sources whose addresses differ from dest's mod 16 take the realigned kernel from 1 KiB
+    # (fanin_realign_kernel: aligned loads, a cross-lane shuffle and a funnel shift per source).
+    # Every element-aligned shift of dest and of each source, ragged sizes; bit-exact against the
+    # oracle's fold, and the bytes around dest untouched.
+    from ishmem_amd import hip
+    es = np.dtype(oracle.NP[dt]).itemsize
+    op = oracle.OPS["sum"]
+    offs_all = list(range(0, 16, es))
+    n_max = 70_001
+    pad = 64
+    base = [hip.malloc(n_max * es + 2 * pad) for _ in range(3)]
+    rng = np.random.default_rng(dt)
+    for n in (256 // es + 3, 4099, n_max):
+        for _ in range(6):
+            o = [int(rng.choice(offs_all)) for _ in range(3)]
+            srcs = [oracle.fill_random(dt, n + 7 * i + o[i], n) for i in range(2)]
+            hip.upload(base[0] + pad + o[0], srcs[0])
+            hip.upload(base[1] + pad + o[1], srcs[1])
+            hip.memset(base[2], 0xA5, n_max * es + 2 * pad)
+            assert ish.combine("sum", DNAMES[dt], base[2] + pad + o[2],
+                               [base[0] + pad + o[0], base[1] + pad + o[1]], n) == 0, ish.last_error()
+            hip.synchronize()
+            got = hip.download(base[2] + pad + o[2], n, oracle.NP[dt])
+            assert _bits_equal(got, oracle.reduce_fold(op, dt, srcs, 0)), (dt, n, o)
+            raw = hip.download(base[2], n_max * es + 2 * pad, np.uint8)
+            lo, hi = pad + o[2], pad + o[2] + n * es
+            assert (raw[:lo] == 0xA5).all() and (raw[hi:] == 0xA5).all(), (dt, n, o)
+    for p in base:
+        hip.free(p)
+
+
+@pytest.mark.parametrize("dtype,es", [("uint8", 1), ("float", 4), ("double", 8)])
+def test_single_pe_reduce_realigned_copy(ish, dtype, es):
+    # The 1-PE reduce is a copy (reduce_impl.h:288-289); with source and dest on different 16-B
+    # phases it is a byte copy through the realigned kernel.  Every (dest, source) phase pair of
+    # the element size at two ragged sizes, the bytes around dest untouched.
+    from ishmem_amd import hip
+    npd = np.dtype(dtype)
+    pad = 64
+    for n in (1024 // es + 5, 300_007):
+        nb = n * es + 2 * pad
+        s_buf, d_buf = ish.ishmem_malloc(nb), ish.ishmem_malloc(nb)
+        x = np.random.default_rng(n).integers(0, 256, n * es, dtype=np.uint8).view(npd)
+        for so in range(0, 16, es):
+            for do in range(0, 16, es):
+                if (so - do) % 16 == 0 and so != 0:
+                    continue  # same phase: the vector path, covered elsewhere
+                hip.upload(s_buf + pad + so, x)
+                hip.memset(d_buf, 0x5A, nb)
+                assert ish.reduce_on_stream("sum" if dtype != "uint8" else "or", dtype, d_buf + pad + do,
+                                            s_buf + pad + so, n, None, 0) == 0, ish.last_error()
+                hip.synchronize()
+                raw = hip.download(d_buf, nb, np.uint8)
+                got = raw[pad + do: pad + do + n * es]
+                assert np.array_equal(got, x.view(np.uint8)), (dtype, n, so, do)
+                assert (raw[:pad + do] == 0x5A).all() and (raw[pad + do + n * es:] == 0x5A).all(), (so, do)
+        ish.ishmem_free(d_buf)
+        ish.ishmem_free(s_buf)
+
+
 def test_single_pe_reduce_is_copy(ish):
     from ishmem_amd import hip
     n = 1_000_003
