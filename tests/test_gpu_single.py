@@ -108,7 +108,7 @@ def test_single_pe_reduce_realigned_copy(ish, dtype, es):
     # phases it is a byte copy through the realigned kernel.  Every (dest, source) phase pair of
     # the element size at two ragged sizes, the bytes around dest untouched.
     from ishmem_amd import hip
-    npd = np.dtype(dtype)
+    npd = {"uint8": np.uint8, "float": np.float32, "double": np.float64}[dtype]  # np.dtype("float") is f64
     pad = 64
     for n in (1024 // es + 5, 300_007):
         nb = n * es + 2 * pad
