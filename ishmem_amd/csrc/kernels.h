@@ -181,6 +181,11 @@ struct PhaseArgs {
     // loads instead of system-coherent (sc0 sc1) ones, leaning on the kernel-boundary acquire for
     // visibility.  For the N > 1 bench's A/B over xGMI (speed, and the tripwire for coherence).
     int peer_nt;
+    // Sources on another 16-B phase than dest (runtime.cpp reduce_heap): the byte shift of every
+    // member's source at the first dest vector (head = elements until dest is 16-B aligned), and
+    // the payload bytes that bound the realigned loads; 0 = same phase.
+    uint32_t shift;
+    uint64_t total;
 };
 hipError_t launch_rs_phase(int op, int dt, const PhaseArgs &a, hipStream_t s);
 hipError_t launch_ag_phase(const PhaseArgs &a, hipStream_t s);

@@ -995,22 +995,31 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4 &A, const u32x4 &B, uint32
     }
 }
 
-template <typename T>
-__device__ __forceinline__ Vec<T> realigned_load(const FaninArgs &a, int j, uint64_t wo, uint32_t tid)
+// The 16 bytes at src0 + wo + 16 * tid, where src0 + wo sits k bytes past the 16-B grid (k
+// uniform): one aligned load per lane (cache policy AUX), the neighbour's by a shuffle, a funnel.
+// Every lane of the wave must call it (the shuffle); `total` bounds the loads at the source's
+// end rounded up to 16 B.
+template <typename T, int AUX>
+__device__ __forceinline__ Vec<T> realigned_vec(const char *src0, uint64_t total, uint64_t wo, uint32_t k,
+                                               uint32_t tid)
 {
-    const uint32_t k = a.shift[j];
-    const uint64_t start = wo - k;  // 16-B aligned in memory (dst + wo is, src + wo has residue k)
-    const char *sb = uniform_ptr(a.src[j] + start);
-    const uint64_t end_al = (((uint64_t) (uintptr_t) a.src[j] + a.total + 15) & ~15ull) - (uint64_t) (uintptr_t) sb;
+    const char *sb = uniform_ptr(src0 + (wo - k));  // 16-B aligned in memory
+    const uint64_t end_al = (((uint64_t) (uintptr_t) src0 + total + 15) & ~15ull) - (uint64_t) (uintptr_t) sb;
     const __amdgpu_buffer_rsrc_t r = make_rsrc_n(sb, end_al);
-    const u32x4 A = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, kNonTemporal);
+    const u32x4 A = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, AUX);
     u32x4 B;
     B.x = __shfl_down(A.x, 1u);
     B.y = __shfl_down(A.y, 1u);
     B.z = __shfl_down(A.z, 1u);
     B.w = __shfl_down(A.w, 1u);
-    if (tid == kFaninBlock - 1) B = __builtin_amdgcn_raw_buffer_load_b128(r, kFaninBlock * 16u, 0, kNonTemporal);
+    if (tid == kFaninBlock - 1) B = __builtin_amdgcn_raw_buffer_load_b128(r, kFaninBlock * 16u, 0, AUX);
     return __builtin_bit_cast(Vec<T>, funnel16(A, B, k));
+}
+
+template <typename T>
+__device__ __forceinline__ Vec<T> realigned_load(const FaninArgs &a, int j, uint64_t wo, uint32_t tid)
+{
+    return realigned_vec<T, kNonTemporal>(a.src[j], a.total, wo, a.shift[j], tid);
 }
 
 template <typename T, int OP, int NS>
@@ -1123,8 +1132,27 @@ __global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
             else rs_phase_item_any<T, OP>(a, wb, valid);
         }
     };
-    if (a.peer_nt) body(std::true_type{});
-    else body(std::false_type{});
+    if (a.shift) {
+        // Sources on another 16-B phase than dest (every member's source has the same one: the
+        // offsets are symmetric): realigned loads (kernels_impl.h realigned_vec), members folded
+        // in team order.  Every lane loads, so the shuffles see their neighbours; valid lanes store.
+        for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kFaninBlock; i0 < ce; i0 += stride) {
+            const uint64_t wb = head_bytes + i0 * 16;
+            const uint32_t tid = threadIdx.x;
+            Vec<T> acc;
+            for (int j = 0; j < p; ++j) {
+                const Vec<T> x = (j == me || a.peer_nt)
+                                     ? realigned_vec<T, kNonTemporal>(a.src[j], a.total, wb, a.shift, tid)
+                                     : realigned_vec<T, kSysCoherent>(a.src[j], a.total, wb, a.shift, tid);
+                acc = j == 0 ? x : op1<T, OP>(acc, x);
+            }
+            if (i0 + tid < ce) wt_store(make_rsrc(uniform_ptr(a.dst + wb)), tid * 16u, acc);
+        }
+    } else if (a.peer_nt) {
+        body(std::true_type{});
+    } else {
+        body(std::false_type{});
+    }
     // Unaligned head (member 0's) and tail (member p-1's), element-wise, by workgroup 0;
     // descriptors based at the region (offsets < 16 B).
     if (blockIdx.x == 0) {

@@ -647,7 +647,11 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     // Not in place (a member would overwrite its source while the peer still reads it).  The
     // choice depends only on symmetric-address properties, so every member makes the same one.
     const uintptr_t d0 = (uintptr_t) dst, s0 = (uintptr_t) src, nb = n * es;
-    if (pl.vec && (long long) nb >= s.phased_min) {
+    // Source and dest on different 16-B phases (same on every PE: the offsets are symmetric): the
+    // phased grids realign the sources (rs_phase_kernel, a.shift) instead of the persistent
+    // kernel's element-granular path.
+    const bool realign = !pl.vec && d0 % es == 0 && s0 % es == 0 && nb >= kRealignMinBytes;
+    if ((pl.vec || realign) && (long long) nb >= s.phased_min) {
         // From phased_min bytes: barrier, one-shot reduce-scatter, barrier, one-shot all-gather,
         // barrier (kernels_impl.h, "Phased reduce-scatter + all-gather").  The barriers carry *ret.
         // Checked before the two-member one-shot fold, which it beats from 32 MiB.
@@ -666,6 +670,15 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         ph.p = t.size;
         ph.me = t.my_idx;
         ph.peer_nt = s.phased_peer_nt;
+        if (realign) {
+            const uint64_t h = std::min<uint64_t>(n, ((16 - d0 % 16) % 16) / es);
+            ph.head = h;
+            ph.nitems = (n - h) * es / 16;
+            ph.tail = n - h - ph.nitems * (16 / es);
+            ph.items_per_chunk = items_per_chunk(ph.nitems, t.size);
+            ph.shift = (uint32_t) ((s0 + h * es) % 16);
+            ph.total = nb;
+        }
         const bool ev = s.phase_events && !capturing(st);
         auto mark = [&](int k) -> int {
             if (ev) HIP_TRY(hipEventRecord(s.phase_ev[k], st));

@@ -344,6 +344,38 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 ish.ishmem_free(base_d)
                 ish.ishmem_free(base_s)
 
+        if "offsets_large" in scenarios:
+            # Source and dest on different 16-B phases at sizes past the vector threshold: the
+            # phased reduce-scatter realigns the sources (rs_phase_kernel, PhaseArgs::shift), the
+            # persistent kernel runs element-granular; both against the oracle, the guard bytes
+            # around dest untouched.
+            for dt in (DT["int8"], DT["float"], DT["double"]):
+                es = np.dtype(oracle.NP[dt]).itemsize
+                nmax = 262_147
+                base_s, base_d = heap(nmax + 64, dt), heap(nmax + 64, dt)
+                for nelems in (1027, 70_001, nmax):
+                    for so, do in ((es, 0), (0, 3 * es % 16), (8 % 16, 12 % 16), (15 - 15 % es, es)):
+                        so, do = so - so % es, do - do % es
+                        if (so - do) % 16 == 0:
+                            continue
+                        op = OPS["sum"] if dt >= 8 else OPS["max"]
+                        ins = [oracle.fill_random(dt, 2000 + 11 * j + nelems + so, nelems) for j in range(npes)]
+                        hip.upload(base_s + 16 + so, ins[pe])
+                        hip.memset(base_d, 0x3C, (nmax + 64) * es)
+                        ish.ishmem_barrier_all()
+                        r = ish.reduce(ONAMES[op], NAMES[dt], base_d + 16 + do, base_s + 16 + so, nelems)
+                        if r:
+                            fails.append(f"pe{pe} offsets_large rc={r} {ish.last_error()}")
+                            continue
+                        check(f"offsets_large dt{dt} n{nelems} so{so} do{do}", op, dt, ins,
+                              hip.download(base_d + 16 + do, nelems, oracle.NP[dt]))
+                        raw = hip.download(base_d, (nmax + 64) * es, np.uint8)
+                        lo, hi = 16 + do, 16 + do + nelems * es
+                        if not ((raw[:lo] == 0x3C).all() and (raw[hi:] == 0x3C).all()):
+                            fails.append(f"pe{pe} offsets_large dt{dt} n{nelems} so{so} do{do}: guard bytes written")
+                ish.ishmem_free(base_d)
+                ish.ishmem_free(base_s)
+
         if "edge" in scenarios:
             s, d = heap(16, DT["float"]), heap(16, DT["float"])
             if ish.ishmem_float_sum_reduce(d, s, 0) != 0:  # nreduce == 0 still synchronises

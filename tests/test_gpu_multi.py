@@ -65,7 +65,7 @@ def test_all_ops_types_vs_oracle_and_mpich_golden(npes, ll):
 @pytest.mark.parametrize("npes", [2, 3])
 @pytest.mark.parametrize("ll", ["on", "off"])
 def test_inplace_offsets_edges(npes, ll):
-    run_pes(npes, ["inplace", "offsets", "edge"], env={"ISHMEM_LL_MAX_BYTES": 65536 if ll == "on" else 0})
+    run_pes(npes, ["inplace", "offsets", "offsets_large", "edge"], env={"ISHMEM_LL_MAX_BYTES": 65536 if ll == "on" else 0})
 
 
 def test_stream_staged_team():
@@ -160,7 +160,7 @@ def test_phased_reduce_scatter_allgather_path(npes):
     # the golden inputs (every op / type), in place, the offset sweep (head / tail elements, empty
     # chunks), edge cases, 256 MiB per PE compared in full, hipGraph replay and the chained-
     # producer coherence tripwire.  p = 3 runs the run-time team-size fold.
-    run_pes(npes, ["phaseevents", "golden", "inplace", "offsets", "edge", "large", "graph", "tripwire"],
+    run_pes(npes, ["phaseevents", "golden", "inplace", "offsets", "offsets_large", "edge", "large", "graph", "tripwire"],
             env={"ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_ONESHOT_P2_MAX_BYTES": 0,
                  "ISHMEM_MAX_BLOCKS": 64},
             timeout=400)
@@ -172,7 +172,7 @@ def test_phased_path_with_nontemporal_peer_loads(npes):
     # set_param "phased_peer_nt": the phased grids load peers' bytes nontemporal instead of sc0 sc1,
     # relying on the kernel-boundary acquire).  On one GPU it must give the same bytes; whether it
     # stays coherent across devices is what the bench's tripwire_peer_nt leg records on the node.
-    run_pes(npes, ["golden", "inplace", "offsets", "large", "tripwire"],
+    run_pes(npes, ["golden", "inplace", "offsets", "offsets_large", "large", "tripwire"],
             env={"ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_ONESHOT_P2_MAX_BYTES": 0,
                  "ISHMEM_PHASED_PEER_NT": 1, "ISHMEM_MAX_BLOCKS": 64},
             timeout=400)
