@@ -966,7 +966,7 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
 
 // ---------------------------------------------------------------------------------------------
 // Realigned fan-in: 1 or 2 sources whose addresses differ from dst's mod 16, every operand
-// element-aligned (runtime.cpp plan_realign).  The element-granular path moved such operands one
+// element-aligned (runtime.cpp plan_fanin).  The element-granular path moved such operands one
 // element per lane — a 1-PE reduce (a byte copy) at 0.6 TB/s, a + b at 3.4 TB/s on 256 MiB
 // (tools/misaligned_probe.py).  Here dst is peeled to the 16-B grid (head elements, workgroup 0)
 // and every lane loads the ALIGNED 16-B vector of each source at its item, takes its neighbour
