@@ -153,6 +153,19 @@ hipError_t launch_scan_direct(int dt, const ScanArgs &a, bool vec, hipStream_t s
 
 // Arguments of the local k-input fan-in combine: dst = op(src0, src1, ..., src_{k-1}).
 constexpr int kMaxFanin = 16;
+// Realigned fan-in: 1 KiB blocks per workgroup (kernels_impl.h fanin_realign_kernel).  Each
+// workgroup's last block loads one vector of the next workgroup's first line.
+#ifndef ISHMEMI_REALIGN_BLOCKS
+#define ISHMEMI_REALIGN_BLOCKS 1
+#endif
+constexpr int kRealignBlocks = ISHMEMI_REALIGN_BLOCKS;
+// Dest alignment the realigned body starts at (the head before it runs element-wise): 256 B, so
+// the workgroups' 1 KiB store blocks cover whole lines instead of sharing one with a neighbour.
+#ifndef ISHMEMI_REALIGN_PEEL
+#define ISHMEMI_REALIGN_PEEL 256
+#endif
+constexpr uint64_t kRealignPeel = ISHMEMI_REALIGN_PEEL;
+
 struct FaninArgs {
     const char *src[kMaxFanin];
     char *dst;

@@ -1022,12 +1022,67 @@ __device__ __forceinline__ Vec<T> realigned_load(const FaninArgs &a, int j, uint
     return realigned_vec<T, kNonTemporal>(a.src[j], a.total, wo, a.shift[j], tid);
 }
 
+// One aligned source vector per lane of block `blk` (1 KiB of dest) of source j.
+template <int AUX>
+__device__ __forceinline__ u32x4 realign_block_load(const FaninArgs &a, int j, uint64_t hb, uint64_t blk,
+                                                    uint32_t lane_off)
+{
+    const uint64_t wo = hb + blk * (kFaninBlock * 16ull);
+    const char *sb = uniform_ptr(a.src[j] + (wo - a.shift[j]));
+    const uint64_t end_al = (((uint64_t) (uintptr_t) a.src[j] + a.total + 15) & ~15ull) - (uint64_t) (uintptr_t) sb;
+    return __builtin_amdgcn_raw_buffer_load_b128(make_rsrc_n(sb, end_al), lane_off, 0, AUX);
+}
+
 template <typename T, int OP, int NS>
 __global__ __launch_bounds__(kFaninBlock) void fanin_realign_kernel(FaninArgs a)
 {
     static_assert(NS == 1 || NS == 2, "realigned fan-in: 1 or 2 sources");
     const uint32_t tid = threadIdx.x;
     const uint64_t hb = a.head * sizeof(T);
+#if ISHMEMI_REALIGN_BLOCKS > 1
+    // kRealignBlocks consecutive 1 KiB blocks per workgroup: block b+1's vectors are loaded
+    // before block b is shifted, and lane 63 takes its neighbour from lane 0 of those, so only
+    // the workgroup's last block reaches into the next workgroup's first line.
+    const uint64_t nblk = (a.nitems + kFaninBlock - 1) / kFaninBlock;
+    for (uint64_t b0 = (uint64_t) blockIdx.x * kRealignBlocks; b0 < nblk; b0 += (uint64_t) gridDim.x * kRealignBlocks) {
+        u32x4 A[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) A[j] = realign_block_load<kNonTemporal>(a, j, hb, b0, tid * 16u);
+#pragma unroll
+        for (int u = 0; u < kRealignBlocks; ++u) {
+            const uint64_t b = b0 + u;
+            if (b >= nblk) break;
+            const bool more = u + 1 < kRealignBlocks && b + 1 < nblk;
+            Vec<T> x[NS];
+            u32x4 An[NS];
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                u32x4 B;
+                B.x = __shfl_down(A[j].x, 1u);
+                B.y = __shfl_down(A[j].y, 1u);
+                B.z = __shfl_down(A[j].z, 1u);
+                B.w = __shfl_down(A[j].w, 1u);
+                if (more) {
+                    An[j] = realign_block_load<kNonTemporal>(a, j, hb, b + 1, tid * 16u);
+                    const u32x4 f = {(uint32_t) __builtin_amdgcn_readfirstlane(An[j].x), (uint32_t) __builtin_amdgcn_readfirstlane(An[j].y),
+                                     (uint32_t) __builtin_amdgcn_readfirstlane(An[j].z), (uint32_t) __builtin_amdgcn_readfirstlane(An[j].w)};
+                    if (tid == kFaninBlock - 1) B = f;
+                } else if (tid == kFaninBlock - 1) {
+                    B = realign_block_load<kNonTemporal>(a, j, hb, b, kFaninBlock * 16u);
+                }
+                x[j] = __builtin_bit_cast(Vec<T>, funnel16(A[j], B, a.shift[j]));
+            }
+            Vec<T> acc = x[0];
+            if constexpr (NS == 2) acc = op1<T, OP>(acc, x[1]);
+            const uint64_t i0 = b * kFaninBlock;
+            if (i0 + tid < a.nitems) wt_store(make_rsrc(uniform_ptr(a.dst + hb + i0 * 16)), tid * 16u, acc);
+            if (more) {
+#pragma unroll
+                for (int j = 0; j < NS; ++j) A[j] = An[j];
+            }
+        }
+    }
+#else
     const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
     for (uint64_t i0 = (uint64_t) blockIdx.x * kFaninBlock; i0 < a.nitems; i0 += stride) {
         const uint64_t wo = hb + i0 * 16;  // bytes from element 0 to this workgroup's first item
@@ -1035,14 +1090,17 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_realign_kernel(FaninArgs a)
         if constexpr (NS == 2) acc = op1<T, OP>(acc, realigned_load<T>(a, 1, wo, tid));
         if (i0 + tid < a.nitems) wt_store(make_rsrc(uniform_ptr(a.dst + wo)), tid * 16u, acc);
     }
-    if (blockIdx.x == 0) {  // head elements (dst not yet on the 16-B grid) and tail elements
+#endif
+    if (blockIdx.x == 0) {  // head elements (before dst's kRealignPeel boundary) and tail elements
         const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
         for (int pass = 0; pass < 2; ++pass) {
-            if ((uint64_t) tid >= (pass == 0 ? a.head : a.tail)) continue;
-            const uint64_t e = pass == 0 ? (uint64_t) tid : tail_off + tid;
-            T acc = ((const T *) a.src[0])[e];
-            if constexpr (NS == 2) acc = op1<T, OP>(acc, ((const T *) a.src[1])[e]);
-            ((T *) a.dst)[e] = acc;
+            const uint64_t cnt = pass == 0 ? a.head : a.tail;
+            for (uint64_t t = tid; t < cnt; t += kFaninBlock) {
+                const uint64_t e = pass == 0 ? t : tail_off + t;
+                T acc = ((const T *) a.src[0])[e];
+                if constexpr (NS == 2) acc = op1<T, OP>(acc, ((const T *) a.src[1])[e]);
+                ((T *) a.dst)[e] = acc;
+            }
         }
     }
 }

@@ -500,14 +500,15 @@ void plan_fanin(FaninArgs &f, Plan &pl, const void *dst, const void *const *srcs
     bool ok = !pl.vec && nsrc >= 1 && nsrc <= 2 && n * es >= kRealignMinBytes && d % es == 0;
     for (int j = 0; ok && j < nsrc; ++j) ok = (uintptr_t) srcs[j] % es == 0;
     if (!ok) return;
-    const uint64_t h = std::min<uint64_t>(n, ((16 - d % 16) % 16) / es);
+    const uint64_t h = std::min<uint64_t>(n, ((kRealignPeel - d % kRealignPeel) % kRealignPeel) / es);
     f.head = h;
     f.nitems = (n - h) * es / 16;
     f.tail = n - h - f.nitems * (16 / es);
     for (int j = 0; j < nsrc; ++j) f.shift[j] = (uint32_t) (((uintptr_t) srcs[j] + h * es) % 16);
     f.total = n * es;
     f.realign = 1;
-    pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((f.nitems + kFaninBlock - 1) / kFaninBlock,
+    const uint64_t per_wg = (uint64_t) kFaninBlock * kRealignBlocks;
+    pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((f.nitems + per_wg - 1) / per_wg,
                                                              (uint64_t) kFaninMaxGrid));
 }
 

@@ -19,7 +19,7 @@ def main() -> None:
     import ishmem_amd as ish
     from ishmem_amd import hip
     ish.init(0, 1, 0, None)
-    n = (256 << 20) // 4
+    n = (int(os.environ.get("MISALIGNED_MIB", "256")) << 20) // 4
     B = 4 * n + 64
     a, b, d = ish.ishmem_malloc(B), ish.ishmem_malloc(B), ish.ishmem_malloc(B)
     x = np.random.default_rng(1).standard_normal(n + 16).astype(np.float32)
