@@ -226,13 +226,12 @@ def legs_healthy(ish, dist) -> bool:
 
 def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max):
     """BASELINE configs[4]: min/max/prod x int32/float64, 4 KiB .. nbytes_max per PE in steps of 4x:
-    us per call (max over ranks), algbw, and a check of every word up to 64 MiB, above that of
-    4096-element windows at both edges of every member's chunk, the array's end and 8 seeded
-    random places, against the team-order fold of the rotating-winner pattern (selfcheck.pattern:
-    non-periodic, a different value on every PE, the min / max winner rotating over the PEs)."""
+    us per call (max over ranks), algbw, and a check of EVERY word of dest on every rank at every
+    size (the device checker, tests/cpp/pattern_check.hip) against the team-order fold of the
+    rotating-winner pattern (selfcheck.pattern: non-periodic, a different value on every PE, the
+    min / max winner rotating over the PEs)."""
     from ishmem_amd import selfcheck as sc
     out = []
-    rng = np.random.default_rng(5)
     for dtn, npd in (("int32", np.int32), ("double", np.float64)):
         es = np.dtype(npd).itemsize
         nmax = nbytes_max // es
@@ -259,9 +258,9 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max):
                 us, errs = max_over_ranks(dist, [e0.elapsed_ms(e1) * 1000.0 / it, device_errors(ish)])
                 if errs:  # every rank sees the same max: all stop here together
                     raise RuntimeError(f"device timeouts at {op} {dtn} {nb} B: {ish.last_error()}")
-                if nb <= (64 << 20):
+                if sc.checker_kind(npd) == "device" or nb <= (64 << 20):
                     wins = [(0, n)]
-                else:
+                else:  # checker not built: host-side windows (edges of every chunk, the end, random)
                     nitems = nb // 16
                     wins = []
                     for c in range(world):
@@ -270,12 +269,13 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max):
                             lo = max(0, edge * (16 // es) - 2048)
                             wins.append((lo, min(n, lo + 4096) - lo))
                     wins.append((n - 4096, 4096))
-                    wins += [(int(x), 4096) for x in rng.integers(0, n - 4096, 8)]
+                    wins += [(int(x), 4096) for x in np.random.default_rng(5).integers(0, n - 4096, 8)]
                 bad = sum(sc.count_wrong(hip, dst, op, npd, world, lo, m) for lo, m in wins)
                 bad = int(max_over_ranks(dist, [float(bad)])[0])
                 out.append({"op": op, "dtype": dtn, "bytes": nb, "us": round(us, 2),
                             "algbw_GiBps": round(nb / GiB / (us * 1e-6), 2),
-                            "checked": bad == 0, "words_checked": sum(m for _, m in wins)})
+                            "checked": bad == 0, "words_checked": sum(m for _, m in wins),
+                            "checker": sc.checker_kind(npd)})
                 nb *= 4
         ish.ishmem_free(dst)
         ish.ishmem_free(src)
@@ -418,7 +418,8 @@ def rccl_allreduce(dist, device, n, B, world, steps, line, limit_s=240.0):
     """N>1 comparison only: RCCL (torch "nccl" backend) all_reduce of the
     same f32 payload over the same GPUs, after this library has released its heap.  A watchdog
     bounds the leg: if RCCL does not finish within limit_s, rank 0 prints the line already
-    measured (marked) and every rank exits, so the main measurement is never lost."""
+    measured (marked) and every rank exits with status 3, so the main measurement is never lost
+    and the hung leg still shows as a failed run."""
     import threading
 
     import torch
@@ -427,7 +428,8 @@ def rccl_allreduce(dist, device, n, B, world, steps, line, limit_s=240.0):
         if line is not None:
             line["rccl_allreduce"] = {"error": f"did not finish within {limit_s:.0f} s"}
             emit(line)
-        os._exit(0)
+        sys.stdout.flush()
+        os._exit(3)
 
     wd = threading.Timer(limit_s, expire)
     wd.daemon = True
@@ -498,7 +500,7 @@ def cpu_baseline_leg(ish, hip, src, dst, n, B, world, rank, dist, key) -> tuple[
     extra = {}
     if world > 1:
         ns = min(n, (64 << 20) // 4)
-        t = oracle.host_bounce_time(op, dt, ns, rank, world, key + "cpu", src, dst, reps=1)
+        t = oracle.host_bounce_time(op, dt, ns, rank, world, key + "cpu", src, dst, reps=3)
         t = max_over_ranks(dist, [t])[0]
         # The same with MPICH's MPI_Allreduce, N processes one per GPU (rank 0 launches them while
         # the bench ranks wait).
@@ -515,13 +517,13 @@ def cpu_baseline_leg(ish, hip, src, dst, n, B, world, rank, dist, key) -> tuple[
                  "whole_job_GiBps": world * ns * 4 / GiB / t,
                  "sample": f"{world} PEs x {ns * 4 >> 20} MiB f32 sum (a sample of the {B / 2**20:g} "
                            f"MiB payload), one process per GPU, 64 KiB chunks each D2H hipMemcpy -> "
-                           f"shm allreduce -> H2D hipMemcpy (reduce_impl.h:186-228), 1 rep",
+                           f"shm allreduce -> H2D hipMemcpy (reduce_impl.h:186-228), best of 3",
                  "host": host_info()}, extra)
-    t1 = oracle.host_bounce_time(op, dt, n, 0, 1, key + "cpu1", src, dst, reps=1)
+    t1 = oracle.host_bounce_time(op, dt, n, 0, 1, key + "cpu1", src, dst, reps=3)
     cpu = {"value": B / GiB / t1, "unit": "GiB/s", "cores": 1, "kind": "port",
            "sample": f"full workload: 1 PE f32 sum of {B / 2**20:g} MiB, 64 KiB chunks each through "
                      f"a synchronous D2H hipMemcpy, the (1-member) allreduce and a synchronous H2D "
-                     f"hipMemcpy (reduce_impl.h:186-228, memory.cpp:310-321), 1 rep",
+                     f"hipMemcpy (reduce_impl.h:186-228, memory.cpp:310-321), best of 3",
            "host": host_info()}
     side = []
     ns = min(n, (64 << 20) // 4)
@@ -782,7 +784,8 @@ def main() -> int:
     else:
         bad = sc.count_wrong(hip, dst, "sum", np.float32, world, 0, n)
         checked = {"words": n, "mode": "every word, every rank",
-                   "input": "rotating-winner pattern (non-periodic, distinct per PE)"}
+                   "input": "rotating-winner pattern (non-periodic, distinct per PE)",
+                   "checker": sc.checker_kind(np.float32)}
     bad = int(max_over_ranks(dist, [float(bad)])[0])
     if bad:
         raise RuntimeError(f"benchmark result check failed: {bad} words wrong")

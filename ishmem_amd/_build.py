@@ -17,6 +17,10 @@ CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 BUILD = ROOT / "build" / "native"
 LIB = PKG / "libishmem_amd.so"
+# The same library with the runtime's test hooks compiled in (ISHMEM_TEST_PCI_BUS,
+# ISHMEM_TEST_FLAGS_UNAVAILABLE; -DISHMEMI_TEST_HOOKS): loaded only by the GPU tests that emulate
+# one PE per GPU on the one-GPU box (ISHMEM_AMD_LIB).  Shares every kernel object with LIB.
+LIB_TESTHOOKS = PKG / "libishmem_amd_testhooks.so"
 
 # (source, object stem, extra flags): kernels_op.hip is compiled once per reduction op so the
 # ~350 kernel instantiations build in parallel.
@@ -38,9 +42,9 @@ def _deps() -> list[Path]:
 
 
 def needs_build() -> bool:
-    if not LIB.exists():
+    if not LIB.exists() or not LIB_TESTHOOKS.exists():
         return True
-    t = LIB.stat().st_mtime
+    t = min(LIB.stat().st_mtime, LIB_TESTHOOKS.stat().st_mtime)
     return any(p.stat().st_mtime > t for p in _deps())
 
 
@@ -59,7 +63,10 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
               "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in (defines or [])]]
     objs = []
     procs = []
-    for src, stem, extra in SOURCES:
+    sources = list(SOURCES)
+    if out is None:
+        sources.append(("runtime.cpp", "runtime_testhooks", ["-DISHMEMI_TEST_HOOKS=1"]))
+    for src, stem, extra in sources:
         obj = bdir / (stem + ".o")
         objs.append(obj)
         cmd = [hipcc, *common, *extra, "-c", str(CSRC / src), "-o", str(obj)]
@@ -67,15 +74,22 @@ def build(force: bool = False, verbose: bool = False, defines: list[str] | None 
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     for cmd, p in procs:
-        out, _ = p.communicate()
+        out_, _ = p.communicate()
         if p.returncode != 0:
-            raise RuntimeError(f"hipcc failed: {' '.join(cmd)}\n{out.decode(errors='replace')}")
-    tmp = lib.with_suffix(".so.tmp")
-    cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
-    if r.returncode != 0:
-        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout.decode(errors='replace')}")
-    os.replace(tmp, lib)
+            raise RuntimeError(f"hipcc failed: {' '.join(cmd)}\n{out_.decode(errors='replace')}")
+
+    def link(target: Path, objects: list[Path]) -> None:
+        tmp = target.with_suffix(".so.tmp")
+        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objects)]
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout.decode(errors='replace')}")
+        os.replace(tmp, target)
+
+    product = [o for o in objs if o.stem != "runtime_testhooks"]
+    link(lib, product)
+    if out is None:
+        link(LIB_TESTHOOKS, [bdir / "runtime_testhooks.o" if o.stem == "runtime" else o for o in product])
     return lib
 
 

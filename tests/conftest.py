@@ -7,7 +7,8 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 if str(ROOT) not in sys.path:
     sys.path.insert(0, str(ROOT))
-os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# No HSA_ENABLE_IPC_MODE_LEGACY here: libishmem_amd sets it when it loads (runtime.cpp
+# ipc_mode_default), and the multi-process tests remove it from their PEs' environments.
 
 
 def pytest_configure(config):

@@ -25,8 +25,11 @@ def _bits_equal(a, b):
 def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None = None) -> None:
     fails: list[str] = []
     try:
-        for k, v in (env or {}).items():  # a list gives each PE its own value
-            os.environ[k] = str(v[pe] if isinstance(v, list) else v)
+        for k, v in (env or {}).items():  # a list gives each PE its own value, None removes it
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v[pe] if isinstance(v, list) else v)
         import oracle
         import ishmem_amd as ish
         from ishmem_amd import hip
@@ -1092,14 +1095,16 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
 
         if "cfg5" in scenarios:
             # BASELINE configs[4]: min / max / prod x int32 / float64 at 4 KiB * 4^k up to
-            # CFG5_MAX_BYTES (4 GiB) per PE, rotating-winner pattern (selfcheck.pattern).  Up to
-            # 64 MiB every word is compared; above, windows of 4096 elements at both edges of every
-            # member's chunk, the array's end and 16 seeded random places (int: bit-exact; f64
-            # min / max exact, prod folded in team order like the kernels: bit-exact).
+            # CFG5_MAX_BYTES (4 GiB) per PE, rotating-winner pattern (selfcheck.pattern), EVERY
+            # word of dest on every PE compared at every size by the device checker
+            # (tests/cpp/pattern_check.hip; int: bit-exact; f64 min / max exact, prod folded in team
+            # order like the kernels: bit-exact), as the reference's tester compares every element
+            # (test/include/ishmem_tester.h:1178-1281).
             from ishmem_amd import selfcheck as sc
             maxb = int(os.environ.get("CFG5_MAX_BYTES", 4 << 30))
-            rng = np.random.default_rng(55)
             for dtn, npd in (("int32", np.int32), ("double", np.float64)):
+                if sc.checker_kind(npd) != "device":
+                    raise RuntimeError("cfg5: the device pattern checker (build/libpattern_check.so) is not built")
                 es = np.dtype(npd).itemsize
                 nmax = maxb // es
                 s, d = ish.ishmem_malloc(maxb), ish.ishmem_malloc(maxb)
@@ -1110,27 +1115,18 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                     nb = 4096
                     while nb <= maxb:
                         n = nb // es
-                        hip.memset(d, 0xA5, nb)
+                        hip.memset(d, 0xA5, min(nb + 64, maxb))
                         r = ish.reduce(op, dtn, d, s, n)
                         if r:
                             fails.append(f"pe{pe} cfg5 {op} {dtn} {nb} B rc={r} {ish.last_error()}")
                             nb *= 4
                             continue
-                        if nb <= (64 << 20):
-                            wins = [(0, n)]
-                        else:
-                            nitems = nb // 16
-                            wins = []
-                            for c in range(npes):
-                                b0, e0 = ish.chunk_bounds(nitems, npes, c)
-                                for edge in (b0, e0):
-                                    lo = max(0, edge * (16 // es) - 2048)
-                                    wins.append((lo, min(n, lo + 4096) - lo))
-                            wins.append((n - 4096, 4096))
-                            wins += [(int(x), 4096) for x in rng.integers(0, n - 4096, 16)]
-                        bad = sum(sc.count_wrong(hip, d, op, npd, npes, lo, m) for lo, m in wins)
+                        bad = sc.count_wrong(hip, d, op, npd, npes, 0, n, device=True)
                         if bad:
                             fails.append(f"pe{pe} cfg5 {op} {dtn} {nb} B: {bad} bytes wrong")
+                        # the poisoned bytes past n must stay untouched
+                        if nb < maxb and int(np.count_nonzero(hip.download(d + nb, 64, np.uint8) != 0xA5)):
+                            fails.append(f"pe{pe} cfg5 {op} {dtn} {nb} B: wrote past dest's end")
                         nb *= 4
                 ish.ishmem_free(d)
                 ish.ishmem_free(s)

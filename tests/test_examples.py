@@ -39,7 +39,8 @@ def run_example(exe: Path, npes: int, timeout: float = 180) -> list[str]:
     for pe in range(npes):
         env = {**os.environ, "ISHMEM_PE": str(pe), "ISHMEM_NPES": str(npes), "ISHMEM_DEVICE": "0",
                "ISHMEM_BOOTSTRAP_KEY": key, "ISHMEM_MAX_BLOCKS": "32", "ISHMEM_TIMEOUT_MS": "20000",
-               "ISHMEM_SYMMETRIC_SIZE": "512M", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+               "ISHMEM_SYMMETRIC_SIZE": "512M"}
+        env.pop("HSA_ENABLE_IPC_MODE_LEGACY", None)  # set by the library when it loads
         procs.append(subprocess.Popen([str(exe)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                       text=True))
     outs = []
@@ -78,8 +79,10 @@ def test_pi_reduce_under_mpiexec(wrapped):
     MPI_LOCALRANKID (runtime_mpi.cpp:1256-1282's role) and both PEs must see npes == 2 — before
     this, each rank became a one-PE world that "reduced" by copying and still printed SUCCESS."""
     exe = build_example("pi_reduce")
-    env = {k: v for k, v in os.environ.items() if not k.startswith("ISHMEM_") and k not in TORCHRUN_VARS}
-    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    # Nothing but the launcher: no ISHMEM_*, no torchrun variable and no HSA_ENABLE_IPC_MODE_LEGACY
+    # (the box exports it; libishmem_amd sets it when the program loads it, VERDICT r04 next 1).
+    env = {k: v for k, v in os.environ.items()
+           if not k.startswith("ISHMEM_") and k not in TORCHRUN_VARS and k != "HSA_ENABLE_IPC_MODE_LEGACY"}
     cmd = [str(exe)] if not wrapped else ["sh", "-c", '"$0"; exit $?', str(exe)]
     out = subprocess.run([MPIEXEC, "-n", "2", *cmd], env=env, capture_output=True, text=True, timeout=240)
     text = out.stdout + out.stderr

@@ -34,13 +34,36 @@ def build_exe(src: Path = ROOT / "tests/cpp/reduce_patterns.cpp", exe: Path = EX
     return exe
 
 
+CHECK_LIB = ROOT / "build" / "libpattern_check.so"
+
+
+def build_pattern_check() -> Path:
+    """The device pattern checker of the large-size parity checks (tests/cpp/pattern_check.hip ->
+    build/libpattern_check.so, loaded by ishmem_amd/selfcheck.py)."""
+    src = ROOT / "tests/cpp/pattern_check.hip"
+    if CHECK_LIB.exists() and src.stat().st_mtime <= CHECK_LIB.stat().st_mtime:
+        return CHECK_LIB
+    CHECK_LIB.parent.mkdir(parents=True, exist_ok=True)
+    tmp = CHECK_LIB.with_suffix(".so.tmp")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fPIC", "-shared",
+                    str(src), "-o", str(tmp)], check=True)
+    os.replace(tmp, CHECK_LIB)
+    return CHECK_LIB
+
+
+def base_env() -> dict:
+    """The test's environment without HSA_ENABLE_IPC_MODE_LEGACY, which the box exports: the
+    library sets it when a program loads it (runtime.cpp ipc_mode_default)."""
+    return {k: v for k, v in os.environ.items() if k != "HSA_ENABLE_IPC_MODE_LEGACY"}
+
+
 def run_exe(exe: Path, npes: int, timeout: float = 600) -> None:
     key = f"cpp{uuid.uuid4().hex[:10]}"
     procs = []
     for pe in range(npes):
-        env = {**os.environ, "ISHMEM_PE": str(pe), "ISHMEM_NPES": str(npes), "ISHMEM_DEVICE": "0",
+        env = {**base_env(), "ISHMEM_PE": str(pe), "ISHMEM_NPES": str(npes), "ISHMEM_DEVICE": "0",
                "ISHMEM_BOOTSTRAP_KEY": key, "ISHMEM_MAX_BLOCKS": "32", "ISHMEM_TIMEOUT_MS": "20000",
-               "ISHMEM_SYMMETRIC_SIZE": "512M", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+               "ISHMEM_SYMMETRIC_SIZE": "512M"}
         procs.append(subprocess.Popen([str(exe)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                       text=True))
     outs = []
@@ -92,9 +115,9 @@ def test_reduce_bw_harness_runs_and_checks():
     exe = build_exe(ROOT / "tests/cpp/reduce_bw.cpp", BW_EXE)
     procs = []
     for pe in range(2):
-        env = {**os.environ, "ISHMEM_PE": str(pe), "ISHMEM_NPES": "2", "ISHMEM_DEVICE": "0",
+        env = {**base_env(), "ISHMEM_PE": str(pe), "ISHMEM_NPES": "2", "ISHMEM_DEVICE": "0",
                "ISHMEM_BOOTSTRAP_KEY": key, "ISHMEM_MAX_BLOCKS": "32", "ISHMEM_TIMEOUT_MS": "20000",
-               "ISHMEM_SYMMETRIC_SIZE": "512M", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+               "ISHMEM_SYMMETRIC_SIZE": "512M"}
         procs.append(subprocess.Popen([str(exe), "--csv", "-m", "1024"], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
     outs = [p.communicate(timeout=300)[0] for p in procs]

@@ -9,15 +9,24 @@ import queue
 import sys
 import time
 import uuid
+from pathlib import Path
 
 import pytest
 
 from tests import mp_worker
 
+ROOT = Path(__file__).resolve().parents[1]
+
 pytestmark = pytest.mark.gpu
 
+# The runtime's test hooks (fake device identity, flag memory "unavailable") are compiled into the
+# test build only (ishmem_amd/_build.py LIB_TESTHOOKS); the product library refuses them at init.
+TESTHOOKS = {"ISHMEM_AMD_LIB": str(ROOT / "ishmem_amd" / "libishmem_amd_testhooks.so")}
+
+# HSA_ENABLE_IPC_MODE_LEGACY is removed from every PE's environment (the box exports it): the
+# library's constructor must set it, as for a program launched the reference's way.
 ENV = {"ISHMEM_MAX_BLOCKS": 32, "ISHMEM_TIMEOUT_MS": 20000, "ISHMEM_SYMMETRIC_SIZE": "1G",
-       "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+       "HSA_ENABLE_IPC_MODE_LEGACY": None}
 
 
 def run_pes(npes: int, scenarios: list[str], timeout: float = 240.0, env: dict | None = None):
@@ -195,7 +204,7 @@ def test_one_pe_per_gpu_configuration_emulated(npes):
     # PE sized its persistent grid for the whole GPU, and eight such waiting grids on one device
     # timed out in the tripwire (profiles/r03/phased_share/r03zh_*).  Now every waiting launch takes
     # at most 1 / wait_slots of the device (kernels.h, "Waiting footprint"), so eight fit at once.
-    env = {"ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
+    env = {**TESTHOOKS, "ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
            "ISHMEM_PHASED_MIN_BYTES": "", "PHASED_WANT": 4 << 20}
     run_pes(npes, ["phasedparam", "golden", "inplace", "edge", "large", "graph", "tripwire"], env=env,
             timeout=400)
@@ -208,7 +217,7 @@ def test_opposite_order_collectives_of_two_teams_one_pe_per_gpu_emulated(npes, s
     # (1 / 4 MiB) and phased sizes.  Deadlock-free by construction while the co-located PEs' waiting
     # launches fit the device: 2 per PE here, so 8 co-located PEs need 1/32 each (ISHMEM_WAIT_SLOTS);
     # one PE per GPU (4 hardware queues per process) is covered by the default 16.
-    env = {"ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
+    env = {**TESTHOOKS, "ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
            "ISHMEM_PHASED_MIN_BYTES": "", "ISHMEM_WAIT_SLOTS": slots}
     run_pes(npes, ["opposite"], env=env, timeout=300)
 
@@ -322,7 +331,7 @@ def test_broadcast_setup_surface_and_agreed_paths(npes):
 
 @pytest.mark.parametrize("forced", [False, True])
 def test_coarse_grained_flags_across_devices_refused_at_init(forced):
-    env = {"ISHMEM_TEST_FLAGS_UNAVAILABLE": 1, "ISHMEM_TEST_PCI_BUS": ["fake-bus-0", "fake-bus-1"]}
+    env = {**TESTHOOKS, "ISHMEM_TEST_FLAGS_UNAVAILABLE": 1, "ISHMEM_TEST_PCI_BUS": ["fake-bus-0", "fake-bus-1"]}
     if forced:
         env["ISHMEM_FLAGS_KIND"] = 2
     run_pes(2, ["refuse"], env=env, timeout=120)

@@ -26,7 +26,10 @@ LAUNCH_VARS = ("ISHMEM_PE", "ISHMEM_NPES", "ISHMEM_DEVICE", "ISHMEM_BOOTSTRAP_KE
                "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "PMI_RANK", "PMI_SIZE",
                "MPI_LOCALRANKID", "MPI_LOCALNRANKS", "OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE",
                "OMPI_COMM_WORLD_LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_SIZE", "SLURM_PROCID", "SLURM_NTASKS",
-               "SLURM_NPROCS", "SLURM_LOCALID", "SLURM_JOB_ID", "SLURM_STEP_ID", "SLURM_NTASKS_PER_NODE")
+               "SLURM_NPROCS", "SLURM_LOCALID", "SLURM_JOB_ID", "SLURM_STEP_ID", "SLURM_NTASKS_PER_NODE",
+               "SLURM_STEP_NUM_TASKS", "SLURM_STEP_NUM_NODES", "ISHMEM_ENABLE_GPU_IPC",
+               "ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "ISHMEM_WAIT_SLOTS", "ISHMEM_TEST_PCI_BUS",
+               "ISHMEM_TEST_FLAGS_UNAVAILABLE", "GPU_MAX_HW_QUEUES")
 
 # One process: what ishmemi_c_init would use, then (optionally) the native bootstrap's allgather
 # among the PEs it names.
@@ -73,7 +76,8 @@ def test_launch_info_reads_each_launcher_family():
     got = probe(clean_env(OMPI_COMM_WORLD_RANK=6, OMPI_COMM_WORLD_SIZE=8, OMPI_COMM_WORLD_LOCAL_RANK=6,
                           OMPI_COMM_WORLD_LOCAL_SIZE=8))
     assert (got["pe"], got["npes"], got["dev"], got["launcher"]) == ("6", "8", "6", "openmpi")
-    got = probe(clean_env(SLURM_PROCID=7, SLURM_NTASKS=8, SLURM_LOCALID=7, SLURM_JOB_ID=42))
+    got = probe(clean_env(SLURM_PROCID=7, SLURM_NTASKS=8, SLURM_STEP_NUM_TASKS=8, SLURM_STEP_ID=0,
+                          SLURM_STEP_NUM_NODES=1, SLURM_LOCALID=7, SLURM_JOB_ID=42))
     assert (got["pe"], got["npes"], got["dev"], got["launcher"]) == ("7", "8", "7", "slurm")
     # Explicit variables override the launcher's, one by one.
     got = probe(clean_env(PMI_RANK=1, PMI_SIZE=2, MPI_LOCALRANKID=1, ISHMEM_DEVICE=0))
@@ -85,6 +89,40 @@ def test_launch_info_refuses_multi_node_and_bad_ranks():
     assert got["rc"] == "1" and "one_node" in got["err"], got
     got = probe(clean_env(ISHMEM_PE=3, ISHMEM_NPES=2))
     assert got["rc"] == "1", got
+    # `srun -N2 -n8` without --ntasks-per-node: refused by the step's node count.
+    got = probe(clean_env(SLURM_PROCID=0, SLURM_NTASKS=8, SLURM_STEP_NUM_TASKS=8, SLURM_STEP_ID=3,
+                          SLURM_STEP_NUM_NODES=2, SLURM_LOCALID=0, SLURM_JOB_ID=42))
+    assert got["rc"] == "1" and "2_nodes" in got["err"], got
+
+
+@pytest.mark.parametrize("step", ["batch", "interactive", "extern", None])
+def test_slurm_batch_step_is_a_one_pe_world(step):
+    """inside `sbatch -n 8` the batch script's environment has SLURM_PROCID=0 and
+    SLURM_NTASKS=8 for the allocation; a program started there without srun is one process and must
+    be a 1-PE world, not PE 0 of 8 waiting in the bootstrap for peers that never start.  Only an srun
+    task step (numeric SLURM_STEP_ID, SLURM_STEP_NUM_TASKS) names a multi-PE world."""
+    env = dict(SLURM_PROCID=0, SLURM_NTASKS=8, SLURM_NPROCS=8, SLURM_LOCALID=0, SLURM_JOB_ID=42,
+               SLURM_NTASKS_PER_NODE=8)
+    if step is not None:
+        env["SLURM_STEP_ID"] = step
+    got = probe(clean_env(**env))
+    assert (got["rc"], got["pe"], got["npes"], got["launcher"]) == ("0", "0", "1", "none"), got
+
+
+@pytest.mark.parametrize("name,value", [("ISHMEM_PE", "abc"), ("ISHMEM_NPES", "2x"), ("PMI_RANK", "1.0"),
+                                        ("OMPI_COMM_WORLD_SIZE", "8 8"), ("ISHMEM_DEVICE", "")])
+def test_launch_identity_variables_parse_strictly(name, value):
+    """the identity variables pick the bootstrap world, so a malformed one fails
+    with its name instead of parsing as a prefix (ISHMEM_NPES='2x' -> 2, ISHMEM_PE='abc' -> 0).
+    An empty value counts as unset, as for every other variable."""
+    base = {"ISHMEM_PE": dict(ISHMEM_PE=0, ISHMEM_NPES=2), "ISHMEM_NPES": dict(ISHMEM_PE=0, ISHMEM_NPES=2),
+            "PMI_RANK": dict(PMI_RANK=0, PMI_SIZE=2), "OMPI_COMM_WORLD_SIZE": dict(OMPI_COMM_WORLD_RANK=0),
+            "ISHMEM_DEVICE": dict(ISHMEM_PE=0, ISHMEM_NPES=1)}[name]
+    got = probe(clean_env(**{**base, name: value}))
+    if value:
+        assert got["rc"] == "1" and name in got["err"] and "not_an_integer" in got["err"], got
+    else:
+        assert got["rc"] == "0", got
 
 
 @pytest.mark.skipif(not Path(MPIEXEC).exists(), reason="no mpiexec (MPICH hydra)")
@@ -149,6 +187,14 @@ print("rc=%d|%s" % (rc, L.ishmemi_c_last_error().decode()))
     ("ISHMEM_SYMMETRIC_SIZE", "2T", False), ("ISHMEM_PHASED_MIN_BYTES", "-1", False),
     # integer variables: the same rule (a prefix such as "16x" -> 16 used to pass silently)
     ("ISHMEM_WAIT_SLOTS", "16x", True), ("ISHMEM_STAGING_SLOTS", "four", True),
+    # the waiting-footprint floor: below GPU_MAX_HW_QUEUES (4) fails init
+    ("ISHMEM_WAIT_SLOTS", "1", True), ("ISHMEM_WAIT_SLOTS", "3", True), ("ISHMEM_WAIT_SLOTS", "4", False),
+    # reference switches this IPC-only path cannot honour, refused by name
+    ("ISHMEM_ENABLE_GPU_IPC", "0", True), ("ISHMEM_ENABLE_GPU_IPC", "false", True),
+    ("ISHMEM_ENABLE_GPU_IPC", "1", False), ("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "1", True),
+    ("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "FALSE", False), ("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "0", False),
+    # test hooks exist only in libishmem_amd_testhooks.so
+    ("ISHMEM_TEST_PCI_BUS", "fake-bus-0", True), ("ISHMEM_TEST_FLAGS_UNAVAILABLE", "1", True),
     ("ISHMEM_TIMEOUT_MS", "99999999999999999999", True), ("ISHMEM_FLAGS_KIND", "1.5", True),
     ("ISHMEM_MAX_BLOCKS", " 256 ", False), ("ISHMEM_TIMEOUT_MS", "-5", False)])
 def test_byte_count_variables_parse_strictly(name, value, bad):
@@ -165,3 +211,41 @@ def test_byte_count_variables_parse_strictly(name, value, bad):
         assert line.startswith("rc=1|") and name in line, line
     else:
         assert name not in line, line
+
+
+def test_wait_slots_floor_follows_hw_queues():
+    """The floor is GPU_MAX_HW_QUEUES: with 8 queues per process, 6 slots are refused."""
+    out = subprocess.run([sys.executable, "-c", ENV_PROBE, str(ROOT)],
+                         env=clean_env(ISHMEM_WAIT_SLOTS=6, GPU_MAX_HW_QUEUES=8), capture_output=True, text=True,
+                         timeout=120)
+    line = out.stdout.strip().splitlines()[-1]
+    assert line.startswith("rc=1|") and "ISHMEM_WAIT_SLOTS=6 is below 8" in line, line
+
+
+IPC_ENV_PROBE = r'''
+import ctypes, os, sys
+sys.path.insert(0, sys.argv[1])
+from ishmem_amd import _lib
+_lib.load(build_if_missing=False)
+libc = ctypes.CDLL(None)
+libc.getenv.restype = ctypes.c_char_p
+v = libc.getenv(b"HSA_ENABLE_IPC_MODE_LEGACY")
+print("value=" + (v.decode() if v is not None else "unset"))
+'''
+
+
+@pytest.mark.parametrize("preset,want", [(None, "0"), ("1", "1"), ("0", "0")])
+def test_library_sets_ipc_mode_when_loaded(preset, want):
+    """VERDICT r04 next 1: the drop-in program launched the reference's way sets no HSA variable, and
+    this node's driver shares device memory as dma-buf only; the library's constructor sets
+    HSA_ENABLE_IPC_MODE_LEGACY=0 when it is loaded (before any HIP call of a program linked against
+    it) and leaves a user's own value alone.  The GPU side: test_pi_reduce_under_mpiexec and
+    test_gpu_multi.py::test_two_pes_without_ipc_mode_variable run with the variable removed."""
+    env = clean_env()
+    env.pop("HSA_ENABLE_IPC_MODE_LEGACY", None)
+    if preset is not None:
+        env["HSA_ENABLE_IPC_MODE_LEGACY"] = preset
+    out = subprocess.run([sys.executable, "-c", IPC_ENV_PROBE, str(ROOT)], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == f"value={want}", out.stdout

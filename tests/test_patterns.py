@@ -99,3 +99,40 @@ def test_checker_catches_truncated_64bit_tile_base():
     hi = sc.pattern_expected("sum", np.float32, p, 1 << 30, m)
     lo = sc.pattern_expected("sum", np.float32, p, 0, m)
     assert np.count_nonzero(hi != lo) > m // 2
+
+
+NPD_CODES = {np.int32: 2, np.int64: 3, np.uint32: 6, np.uint64: 7, np.float32: 8, np.float64: 9}
+
+
+@pytest.fixture(scope="module")
+def checker():
+    from tests.test_gpu_cpp import build_pattern_check
+    build_pattern_check()
+    sc._checker = None
+    lib = sc.device_checker()
+    assert lib is not None
+    return lib
+
+
+@pytest.mark.parametrize("npd", [np.int32, np.uint32, np.int64, np.float32, np.float64])
+@pytest.mark.parametrize("p", [1, 2, 3, 8])
+@pytest.mark.parametrize("lo,m", [(0, 3000), ((1 << 32) - 700, 1500), (12_345_678_901, 777)])
+def test_device_checker_host_twins_equal_numpy(checker, npd, p, lo, m):
+    """The device checker's pattern and expected fold (tests/cpp/pattern_check.hip, compiled for the
+    host as well) equal selfcheck's numpy, which test_expected_equals_team_order_fold pins to an
+    explicit fold.  int64 products: the true wrap mod 2^64 (selfcheck's numpy only serves 32-bit
+    integer products, the configs[4] dtypes), checked against an explicit int64 fold."""
+    import ctypes
+    code = NPD_CODES[npd]
+    for pe in range(p):
+        got = np.empty(m, npd)
+        assert checker.pc_host_pattern(got.ctypes.data_as(ctypes.c_void_p), code, pe, p, lo, m) == 0
+        assert np.array_equal(got, sc.pattern(pe, p, lo, m, npd))
+    for op, opc in (("sum", 5), ("min", 4), ("max", 3), ("prod", 6)):
+        got = np.empty(m, npd)
+        assert checker.pc_host_expected(got.ctypes.data_as(ctypes.c_void_p), opc, code, p, lo, m) == 0
+        if op == "prod" and np.dtype(npd).itemsize == 8 and np.issubdtype(npd, np.integer):
+            want = fold(op, npd, [sc.pattern(pe, p, lo, m, npd) for pe in range(p)])
+        else:
+            want = sc.pattern_expected(op, npd, p, lo, m)
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (op, npd, p, lo)

@@ -20,7 +20,8 @@ from tests.test_gpu_multi import run_pes  # noqa: E402
 def main() -> int:
     npes = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     slots = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    env = {"ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
+    env = {"ISHMEM_AMD_LIB": str(Path(__file__).resolve().parents[1] / "ishmem_amd/libishmem_amd_testhooks.so"),
+           "ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
            "ISHMEM_PHASED_MIN_BYTES": "", "ISHMEM_WAIT_SLOTS": slots, "ISHMEM_TIMEOUT_MS": 3000}
     t0 = time.monotonic()
     try:
