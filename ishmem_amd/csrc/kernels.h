@@ -153,12 +153,15 @@ hipError_t launch_scan_direct(int dt, const ScanArgs &a, bool vec, hipStream_t s
 
 // Arguments of the local k-input fan-in combine: dst = op(src0, src1, ..., src_{k-1}).
 constexpr int kMaxFanin = 16;
-// Realigned fan-in: 1 KiB blocks per workgroup (kernels_impl.h fanin_realign_kernel).  Each
-// workgroup's last block loads one vector of the next workgroup's first line.
-#ifndef ISHMEMI_REALIGN_BLOCKS
-#define ISHMEMI_REALIGN_BLOCKS 1
+// Realigned fan-in (kernels_impl.h fanin_realign_kernel): threads per workgroup, one 16-B dest
+// item each; the workgroup's last lane loads one vector of the next workgroup's first line, so
+// the extra fetch is one line per 8 KiB (round 4's one-wave workgroups: one per 1 KiB).
+#ifndef ISHMEMI_REALIGN_BLOCK
+#define ISHMEMI_REALIGN_BLOCK 512
 #endif
-constexpr int kRealignBlocks = ISHMEMI_REALIGN_BLOCKS;
+constexpr int kRealignBlock = ISHMEMI_REALIGN_BLOCK;
+constexpr int kRealignWaves = kRealignBlock / 64;
+constexpr int kRealignMaxGrid = (int) ((1ull << 31) / kRealignBlock);
 // Dest alignment the realigned body starts at (the head before it runs element-wise): 256 B, so
 // the workgroups' 1 KiB store blocks cover whole lines instead of sharing one with a neighbour.
 #ifndef ISHMEMI_REALIGN_PEEL

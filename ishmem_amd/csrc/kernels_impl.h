@@ -995,107 +995,99 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4 &A, const u32x4 &B, uint32
     }
 }
 
-// The 16 bytes at src0 + wo + 16 * tid, where src0 + wo sits k bytes past the 16-B grid (k
-// uniform): one aligned load per lane (cache policy AUX), the neighbour's by a shuffle, a funnel.
-// Every lane of the wave must call it (the shuffle); `total` bounds the loads at the source's
-// end rounded up to 16 B.
-template <typename T, int AUX>
-__device__ __forceinline__ Vec<T> realigned_vec(const char *src0, uint64_t total, uint64_t wo, uint32_t k,
-                                               uint32_t tid)
+// The neighbour exchange of the realigned fan-in.  A source vector straddles two aligned 16-B
+// vectors: lane i's own and lane i+1's.  Within a wave lane i+1's comes by a DPP wave shift
+// (v_mov_b32_dpp wave_shl:1, four VALU ops, no LDS crossbar traffic); lane 63 takes lane 0 of the
+// next wave through LDS, and the workgroup's last lane loads the vector past the workgroup's end.
+// Round 4's one-wave workgroups did the same with four ds_bpermute shuffles and a boundary load
+// per 1 KiB (0.72 / 0.70 of HBM for copy / a + b at 1 GiB); measured alternatives (tools/
+// realign_variants.hip, 1 GiB, shifts 1 / 4 / 12 B, profiles/r05/realign/): shuffles 0.75 / 0.75,
+// DPP alone 0.75 / 0.76, two aligned loads per lane 0.73 / 0.71, unaligned 16-B loads 0.79 / 0.76
+// (0.80 / 0.82 with an XCD-grouped block order, but 0.77 at a 1-B shift), LDS exchange in 256 /
+// 512-thread workgroups 0.83 / 0.82, DPP + LDS edges in 512-thread workgroups 0.835-0.838 /
+// 0.822-0.827 (aligned kernel 0.84 / 0.83): the boundary load per 8 KiB instead of per 1 KiB, and
+// no shuffle through LDS for 63 of 64 lanes.
+__device__ __forceinline__ u32x4 wave_next(const u32x4 &A)
 {
-    const char *sb = uniform_ptr(src0 + (wo - k));  // 16-B aligned in memory
-    const uint64_t end_al = (((uint64_t) (uintptr_t) src0 + total + 15) & ~15ull) - (uint64_t) (uintptr_t) sb;
-    const __amdgpu_buffer_rsrc_t r = make_rsrc_n(sb, end_al);
-    const u32x4 A = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, AUX);
-    u32x4 B;
-    B.x = __shfl_down(A.x, 1u);
-    B.y = __shfl_down(A.y, 1u);
-    B.z = __shfl_down(A.z, 1u);
-    B.w = __shfl_down(A.w, 1u);
-    if (tid == kFaninBlock - 1) B = __builtin_amdgcn_raw_buffer_load_b128(r, kFaninBlock * 16u, 0, AUX);
-    return __builtin_bit_cast(Vec<T>, funnel16(A, B, k));
+    return u32x4{(uint32_t) __builtin_amdgcn_update_dpp(0, (int) A.x, 0x130, 0xF, 0xF, false),
+                 (uint32_t) __builtin_amdgcn_update_dpp(0, (int) A.y, 0x130, 0xF, 0xF, false),
+                 (uint32_t) __builtin_amdgcn_update_dpp(0, (int) A.z, 0x130, 0xF, 0xF, false),
+                 (uint32_t) __builtin_amdgcn_update_dpp(0, (int) A.w, 0x130, 0xF, 0xF, false)};
 }
 
-template <typename T>
-__device__ __forceinline__ Vec<T> realigned_load(const FaninArgs &a, int j, uint64_t wo, uint32_t tid)
-{
-    return realigned_vec<T, kNonTemporal>(a.src[j], a.total, wo, a.shift[j], tid);
-}
-
-// One aligned source vector per lane of block `blk` (1 KiB of dest) of source j.
+// A realigned load in two steps around a workgroup barrier:
+//   realign_issue  - every thread: the aligned vector A of `src` under this lane for the workgroup
+//                    whose dest starts `wo` bytes past element 0 (src + wo sits `shift` bytes past
+//                    the 16-B grid), its in-wave neighbour B by DPP, each wave's first vector into
+//                    edge[wave] and, from the workgroup's last lane, the vector past the
+//                    workgroup's end into edge[kRealignWaves].  Loads reach at most the source's
+//                    end rounded up to 16 B (the same 16-B block, so the same page); the
+//                    descriptor returns zeros past it;
+//   realign_finish - lane 63 takes the next wave's first vector, then the 16 bytes this lane's
+//                    dest item takes from the source.
+// Sources are issued one after the other, each source's LDS stores waiting for its loads: with
+// two sources that order ran a + b at 0.489-0.490 ms per GiB against 0.511-0.513 ms with both
+// sources' loads issued before any wait (tools/realign_variants.hip var24 / var8, interleaved,
+// profiles/r05/realign/).
 template <int AUX>
-__device__ __forceinline__ u32x4 realign_block_load(const FaninArgs &a, int j, uint64_t hb, uint64_t blk,
-                                                    uint32_t lane_off)
+__device__ __forceinline__ void realign_issue(const char *src, uint32_t shift, uint64_t total, uint64_t wo,
+                                              u32x4 *edge, u32x4 &A, u32x4 &B)
 {
-    const uint64_t wo = hb + blk * (kFaninBlock * 16ull);
-    const char *sb = uniform_ptr(a.src[j] + (wo - a.shift[j]));
-    const uint64_t end_al = (((uint64_t) (uintptr_t) a.src[j] + a.total + 15) & ~15ull) - (uint64_t) (uintptr_t) sb;
-    return __builtin_amdgcn_raw_buffer_load_b128(make_rsrc_n(sb, end_al), lane_off, 0, AUX);
+    const uint32_t tid = threadIdx.x;
+    const char *sb = uniform_ptr(src + (wo - shift));  // 16-B aligned in memory
+    const uint64_t end_al = (((uint64_t) (uintptr_t) src + total + 15) & ~15ull) - (uint64_t) (uintptr_t) sb;
+    const __amdgpu_buffer_rsrc_t r = make_rsrc_n(sb, end_al);
+    A = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, AUX);
+    if (tid == kRealignBlock - 1) edge[kRealignWaves] = __builtin_amdgcn_raw_buffer_load_b128(r, kRealignBlock * 16u, 0, AUX);
+    if ((tid & 63) == 0) edge[tid >> 6] = A;
+    B = wave_next(A);
+}
+
+__device__ __forceinline__ u32x4 realign_finish(const u32x4 *edge, const u32x4 &A, u32x4 B, uint32_t shift)
+{
+    if ((threadIdx.x & 63) == 63) B = edge[(threadIdx.x >> 6) + 1];
+    return funnel16(A, B, shift);
+}
+
+// One 512-item block of the realigned fan-in (every thread; i0 workgroup-uniform).
+template <typename T, int OP, int NS>
+__device__ __forceinline__ void fanin_realign_block(const FaninArgs &a, u32x4 (*edge)[kRealignWaves + 1], uint64_t i0)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t wo = a.head * sizeof(T) + i0 * 16;  // bytes from element 0 to this block's first item
+    u32x4 A[NS], B[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) realign_issue<kNonTemporal>(a.src[j], a.shift[j], a.total, wo, edge[j], A[j], B[j]);
+    __syncthreads();
+    Vec<T> acc = __builtin_bit_cast(Vec<T>, realign_finish(edge[0], A[0], B[0], a.shift[0]));
+    if constexpr (NS == 2)
+        acc = op1<T, OP>(acc, __builtin_bit_cast(Vec<T>, realign_finish(edge[1], A[1], B[1], a.shift[1])));
+    if (i0 + tid < a.nitems) wt_store(make_rsrc(uniform_ptr(a.dst + wo)), tid * 16u, acc);
 }
 
 template <typename T, int OP, int NS>
-__global__ __launch_bounds__(kFaninBlock) void fanin_realign_kernel(FaninArgs a)
+__global__ __launch_bounds__(kRealignBlock) void fanin_realign_kernel(FaninArgs a)
 {
     static_assert(NS == 1 || NS == 2, "realigned fan-in: 1 or 2 sources");
+    __shared__ u32x4 edge[NS][kRealignWaves + 1];
     const uint32_t tid = threadIdx.x;
-    const uint64_t hb = a.head * sizeof(T);
-#if ISHMEMI_REALIGN_BLOCKS > 1
-    // kRealignBlocks consecutive 1 KiB blocks per workgroup: block b+1's vectors are loaded
-    // before block b is shifted, and lane 63 takes its neighbour from lane 0 of those, so only
-    // the workgroup's last block reaches into the next workgroup's first line.
-    const uint64_t nblk = (a.nitems + kFaninBlock - 1) / kFaninBlock;
-    for (uint64_t b0 = (uint64_t) blockIdx.x * kRealignBlocks; b0 < nblk; b0 += (uint64_t) gridDim.x * kRealignBlocks) {
-        u32x4 A[NS];
-#pragma unroll
-        for (int j = 0; j < NS; ++j) A[j] = realign_block_load<kNonTemporal>(a, j, hb, b0, tid * 16u);
-#pragma unroll
-        for (int u = 0; u < kRealignBlocks; ++u) {
-            const uint64_t b = b0 + u;
-            if (b >= nblk) break;
-            const bool more = u + 1 < kRealignBlocks && b + 1 < nblk;
-            Vec<T> x[NS];
-            u32x4 An[NS];
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                u32x4 B;
-                B.x = __shfl_down(A[j].x, 1u);
-                B.y = __shfl_down(A[j].y, 1u);
-                B.z = __shfl_down(A[j].z, 1u);
-                B.w = __shfl_down(A[j].w, 1u);
-                if (more) {
-                    An[j] = realign_block_load<kNonTemporal>(a, j, hb, b + 1, tid * 16u);
-                    const u32x4 f = {(uint32_t) __builtin_amdgcn_readfirstlane(An[j].x), (uint32_t) __builtin_amdgcn_readfirstlane(An[j].y),
-                                     (uint32_t) __builtin_amdgcn_readfirstlane(An[j].z), (uint32_t) __builtin_amdgcn_readfirstlane(An[j].w)};
-                    if (tid == kFaninBlock - 1) B = f;
-                } else if (tid == kFaninBlock - 1) {
-                    B = realign_block_load<kNonTemporal>(a, j, hb, b, kFaninBlock * 16u);
-                }
-                x[j] = __builtin_bit_cast(Vec<T>, funnel16(A[j], B, a.shift[j]));
-            }
-            Vec<T> acc = x[0];
-            if constexpr (NS == 2) acc = op1<T, OP>(acc, x[1]);
-            const uint64_t i0 = b * kFaninBlock;
-            if (i0 + tid < a.nitems) wt_store(make_rsrc(uniform_ptr(a.dst + hb + i0 * 16)), tid * 16u, acc);
-            if (more) {
-#pragma unroll
-                for (int j = 0; j < NS; ++j) A[j] = An[j];
-            }
+    const uint64_t stride = (uint64_t) gridDim.x * kRealignBlock;
+    const uint64_t first = (uint64_t) blockIdx.x * kRealignBlock;
+    if (stride >= a.nitems) {
+        // One block per workgroup (up to 2^31 items = 32 GiB): the grid-stride loop's bookkeeping
+        // cost 1.3 % on the copy (var8, tools/realign_variants.hip).
+        if (first < a.nitems) fanin_realign_block<T, OP, NS>(a, edge, first);
+    } else {
+        for (uint64_t i0 = first; i0 < a.nitems; i0 += stride) {
+            fanin_realign_block<T, OP, NS>(a, edge, i0);
+            __syncthreads();  // edge[] is rewritten by the next pass
         }
     }
-#else
-    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
-    for (uint64_t i0 = (uint64_t) blockIdx.x * kFaninBlock; i0 < a.nitems; i0 += stride) {
-        const uint64_t wo = hb + i0 * 16;  // bytes from element 0 to this workgroup's first item
-        Vec<T> acc = realigned_load<T>(a, 0, wo, tid);
-        if constexpr (NS == 2) acc = op1<T, OP>(acc, realigned_load<T>(a, 1, wo, tid));
-        if (i0 + tid < a.nitems) wt_store(make_rsrc(uniform_ptr(a.dst + wo)), tid * 16u, acc);
-    }
-#endif
     if (blockIdx.x == 0) {  // head elements (before dst's kRealignPeel boundary) and tail elements
         const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
         for (int pass = 0; pass < 2; ++pass) {
             const uint64_t cnt = pass == 0 ? a.head : a.tail;
-            for (uint64_t t = tid; t < cnt; t += kFaninBlock) {
+            for (uint64_t t = tid; t < cnt; t += kRealignBlock) {
                 const uint64_t e = pass == 0 ? t : tail_off + t;
                 T acc = ((const T *) a.src[0])[e];
                 if constexpr (NS == 2) acc = op1<T, OP>(acc, ((const T *) a.src[1])[e]);
@@ -1174,45 +1166,12 @@ __device__ __forceinline__ void rs_phase_item_any(const PhaseArgs &a, uint64_t w
     wt_store(make_rsrc(uniform_ptr(a.dst + wb)), off, acc);
 }
 
-template <typename T, int OP, int P>
-__global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
+// Unaligned head (member 0's) and tail (member p-1's), element-wise, by workgroup 0 of the
+// reduce-scatter grid; descriptors based at the region (offsets < 16 B).
+template <typename T, int OP>
+__device__ __forceinline__ void rs_phase_edges(const PhaseArgs &a)
 {
     const int p = a.p, me = a.me;
-    const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
-    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
-    const uint64_t head_bytes = a.head * sizeof(T);
-    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
-    auto body = [&](auto nt) {
-        for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kFaninBlock; i0 < ce; i0 += stride) {
-            const bool valid = i0 + threadIdx.x < ce;
-            const uint64_t wb = head_bytes + i0 * 16;
-            if constexpr (P > 0) rs_phase_dispatch<T, OP, P, decltype(nt)::value>(a, (int) ((i0 / kFaninBlock) % P), wb, valid);
-            else rs_phase_item_any<T, OP>(a, wb, valid);
-        }
-    };
-    if (a.shift) {
-        // Sources on another 16-B phase than dest (every member's source has the same one: the
-        // offsets are symmetric): realigned loads (kernels_impl.h realigned_vec), members folded
-        // in team order.  Every lane loads, so the shuffles see their neighbours; valid lanes store.
-        for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kFaninBlock; i0 < ce; i0 += stride) {
-            const uint64_t wb = head_bytes + i0 * 16;
-            const uint32_t tid = threadIdx.x;
-            Vec<T> acc;
-            for (int j = 0; j < p; ++j) {
-                const Vec<T> x = (j == me || a.peer_nt)
-                                     ? realigned_vec<T, kNonTemporal>(a.src[j], a.total, wb, a.shift, tid)
-                                     : realigned_vec<T, kSysCoherent>(a.src[j], a.total, wb, a.shift, tid);
-                acc = j == 0 ? x : op1<T, OP>(acc, x);
-            }
-            if (i0 + tid < ce) wt_store(make_rsrc(uniform_ptr(a.dst + wb)), tid * 16u, acc);
-        }
-    } else if (a.peer_nt) {
-        body(std::true_type{});
-    } else {
-        body(std::false_type{});
-    }
-    // Unaligned head (member 0's) and tail (member p-1's), element-wise, by workgroup 0;
-    // descriptors based at the region (offsets < 16 B).
     if (blockIdx.x == 0) {
         const int tid = threadIdx.x;
         const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
@@ -1232,6 +1191,75 @@ __global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
             wt_store(make_rsrc(uniform_ptr(a.dst + rbase)), off, acc);
         }
     }
+}
+
+template <typename T, int OP, int P>
+__global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
+{
+    const int me = a.me;
+    const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
+    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
+    const uint64_t head_bytes = a.head * sizeof(T);
+    const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
+    auto body = [&](auto nt) {
+        for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kFaninBlock; i0 < ce; i0 += stride) {
+            const bool valid = i0 + threadIdx.x < ce;
+            const uint64_t wb = head_bytes + i0 * 16;
+            if constexpr (P > 0) rs_phase_dispatch<T, OP, P, decltype(nt)::value>(a, (int) ((i0 / kFaninBlock) % P), wb, valid);
+            else rs_phase_item_any<T, OP>(a, wb, valid);
+        }
+    };
+    if (a.peer_nt) {
+        body(std::true_type{});
+    } else {
+        body(std::false_type{});
+    }
+    rs_phase_edges<T, OP>(a);
+}
+
+// The phased reduce-scatter with every member's source on another 16-B phase than dest (the same
+// shift on every PE: the offsets are symmetric): the realigned fan-in's loads (realign_issue /
+// realign_finish, 512-thread workgroups, DPP + LDS edges) per member, members taken four at a
+// time — their loads all in flight — and folded in team order.  Round 4 ran this inside
+// rs_phase_kernel's one-wave workgroups with four shuffles and a boundary load per member per
+// 1 KiB.  In place never gets here (source == dest has no shift), so the loads past the chunk's
+// end read only bytes no member writes during the reduce-scatter.
+template <typename T, int OP>
+__global__ __launch_bounds__(kRealignBlock) void rs_phase_realign_kernel(PhaseArgs a)
+{
+    constexpr int G = 4;
+    __shared__ u32x4 edge[G][kRealignWaves + 1];
+    const int p = a.p, me = a.me;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
+    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
+    const uint64_t hb = a.head * sizeof(T);
+    const uint64_t stride = (uint64_t) gridDim.x * kRealignBlock;
+    for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kRealignBlock; i0 < ce; i0 += stride) {
+        const uint64_t wb = hb + i0 * 16;
+        Vec<T> acc;
+        for (int g0 = 0; g0 < p; g0 += G) {
+            u32x4 A[G], B[G];
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                const int j = g0 + k;
+                if (j >= p) break;
+                if (j == me || a.peer_nt) realign_issue<kNonTemporal>(a.src[j], a.shift, a.total, wb, edge[k], A[k], B[k]);
+                else realign_issue<kSysCoherent>(a.src[j], a.shift, a.total, wb, edge[k], A[k], B[k]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                const int j = g0 + k;
+                if (j >= p) break;
+                const Vec<T> x = __builtin_bit_cast(Vec<T>, realign_finish(edge[k], A[k], B[k], a.shift));
+                acc = j == 0 ? x : op1<T, OP>(acc, x);
+            }
+            __syncthreads();
+        }
+        if (i0 + tid < ce) wt_store(make_rsrc(uniform_ptr(a.dst + wb)), tid * 16u, acc);
+    }
+    rs_phase_edges<T, OP>(a);
 }
 
 // Every item outside chunk `me`, pulled from its owner's dest.  Workgroup w takes peer
@@ -1286,7 +1314,11 @@ hipError_t rs_phase_t(const PhaseArgs &a, hipStream_t s)
     auto go = [&](auto kernel) {
         hipLaunchKernelGGL(kernel, dim3(phase_grid(kernel, len)), dim3(kFaninBlock), 0, s, a);
     };
-    if (a.p == 2) go(rs_phase_kernel<T, OP, 2>);
+    if (a.shift) {
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((len + kRealignBlock - 1) / kRealignBlock,
+                                                                    (uint64_t) kRealignMaxGrid));
+        hipLaunchKernelGGL((rs_phase_realign_kernel<T, OP>), dim3((unsigned) g), dim3(kRealignBlock), 0, s, a);
+    } else if (a.p == 2) go(rs_phase_kernel<T, OP, 2>);
     else if (a.p == 4) go(rs_phase_kernel<T, OP, 4>);
     else if (a.p == 8) go(rs_phase_kernel<T, OP, 8>);
     else go(rs_phase_kernel<T, OP, 0>);
@@ -1500,8 +1532,8 @@ template <typename T, int OP>
 hipError_t fi_t(bool vec, const FaninArgs &a, int grid, hipStream_t s)
 {
     if (a.realign) {
-        if (a.nsrc == 1) hipLaunchKernelGGL((fanin_realign_kernel<T, OP, 1>), dim3(grid), dim3(kFaninBlock), 0, s, a);
-        else if (a.nsrc == 2) hipLaunchKernelGGL((fanin_realign_kernel<T, OP, 2>), dim3(grid), dim3(kFaninBlock), 0, s, a);
+        if (a.nsrc == 1) hipLaunchKernelGGL((fanin_realign_kernel<T, OP, 1>), dim3(grid), dim3(kRealignBlock), 0, s, a);
+        else if (a.nsrc == 2) hipLaunchKernelGGL((fanin_realign_kernel<T, OP, 2>), dim3(grid), dim3(kRealignBlock), 0, s, a);
         else return hipErrorInvalidValue;
         return hipGetLastError();
     }

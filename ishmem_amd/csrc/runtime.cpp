@@ -556,9 +556,8 @@ void plan_fanin(FaninArgs &f, Plan &pl, const void *dst, const void *const *srcs
     for (int j = 0; j < nsrc; ++j) f.shift[j] = (uint32_t) (((uintptr_t) srcs[j] + h * es) % 16);
     f.total = n * es;
     f.realign = 1;
-    const uint64_t per_wg = (uint64_t) kFaninBlock * kRealignBlocks;
-    pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((f.nitems + per_wg - 1) / per_wg,
-                                                             (uint64_t) kFaninMaxGrid));
+    pl.grid = (int) std::max<uint64_t>(1, std::min<uint64_t>((f.nitems + kRealignBlock - 1) / kRealignBlock,
+                                                             (uint64_t) kRealignMaxGrid));
 }
 
 int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)

@@ -72,7 +72,7 @@ def test_combine_misaligned_operands(ish, dt):
 @pytest.mark.parametrize("dt", [0, 2, 3, 8, 9])
 def test_combine_realigned_operands(ish, dt):
     # Sources whose addresses differ from dest's mod 16 take the realigned kernel from 1 KiB
-    # (fanin_realign_kernel: aligned loads, a cross-lane shuffle and a funnel shift per source).
+    # (fanin_realign_kernel: aligned loads, a DPP wave shift + LDS edges and a funnel shift per source).
     # Every element-aligned shift of dest and of each source, ragged sizes; bit-exact against the
     # oracle's fold, and the bytes around dest untouched.
     from ishmem_amd import hip
@@ -83,7 +83,9 @@ def test_combine_realigned_operands(ish, dt):
     pad = 64
     base = [hip.malloc(n_max * es + 2 * pad) for _ in range(3)]
     rng = np.random.default_rng(dt)
-    for n in (256 // es + 3, 4099, n_max):
+    # 1024 // es (+1): the realigned kernel's 1 KiB entry point, where the 256-B head peel leaves a
+    # short body and a ragged tail; 8 KiB +- a few: one 512-thread workgroup's span.
+    for n in (256 // es + 3, 1024 // es, 1024 // es + 1, 8192 // es - 3, 8192 // es + 21, 4099, n_max):
         for _ in range(6):
             o = [int(rng.choice(offs_all)) for _ in range(3)]
             srcs = [oracle.fill_random(dt, n + 7 * i + o[i], n) for i in range(2)]
@@ -110,7 +112,7 @@ def test_single_pe_reduce_realigned_copy(ish, dtype, es):
     from ishmem_amd import hip
     npd = {"uint8": np.uint8, "float": np.float32, "double": np.float64}[dtype]  # np.dtype("float") is f64
     pad = 64
-    for n in (1024 // es + 5, 300_007):
+    for n in (1024 // es, 1024 // es + 5, 8192 // es + 1, 300_007):
         nb = n * es + 2 * pad
         s_buf, d_buf = ish.ishmem_malloc(nb), ish.ishmem_malloc(nb)
         x = np.random.default_rng(n).integers(0, 256, n * es, dtype=np.uint8).view(npd)
@@ -225,3 +227,36 @@ def test_on_stream_deps_and_done_event(ish):
     for p in (ret, d, s):
         ish.ishmem_free(p)
     hip.host_free(hx)
+
+
+@pytest.mark.parametrize("npd", [np.int32, np.float64])
+def test_device_pattern_checker_counts_wrong_bytes(ish, npd):
+    """Negative control of the device checker that compares configs[2..4] in every word
+    (tests/cpp/pattern_check.hip via selfcheck.count_wrong): a dest holding the expected fold
+    counts 0 wrong bytes, and exactly the bytes corrupted afterwards are counted — also past 2^32
+    elements of index (the hash's high word) — and the device's answer equals the host check."""
+    from ishmem_amd import hip, selfcheck as sc
+    assert sc.checker_kind(npd) == "device"
+    es = np.dtype(npd).itemsize
+    n = 3_000_001
+    d = ish.ishmem_malloc(n * es)
+    try:
+        for lo in (0, (1 << 32) - 1000):
+            # d holds elements lo .. lo + n of the array, so the array itself starts lo elements
+            # before d (count_wrong checks [lo, lo + m) of the array at `base`).
+            base = d - lo * es
+            # p = 1: the fold of one member is its own pattern (sum / min / max / prod alike)
+            if lo == 0:
+                sc.upload_pattern(hip, d, npd, 0, 1, n)
+            else:
+                hip.upload(d, sc.pattern(0, 1, lo, n, npd))
+            for op in ("sum", "min", "max", "prod"):
+                assert sc.count_wrong(hip, base, op, npd, 1, lo, n) == 0, (op, lo)
+            assert sc.count_wrong(hip, base, "sum", npd, 2, lo, n) > 0  # another team size: wrong
+            hip.memset(d + 5 * es + 1, 0xEE, 3)  # three bytes of element 5
+            hip.memset(d + (n - 1) * es, 0x00, 1)  # the last element's first byte
+            dev = sc.count_wrong(hip, base, "max", npd, 1, lo, n)
+            host = sc.count_wrong(hip, base, "max", npd, 1, lo, n, device=False)
+            assert dev == host and 3 <= dev <= 4, (dev, host)
+    finally:
+        ish.ishmem_free(d)

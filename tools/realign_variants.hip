@@ -13,6 +13,8 @@
 #include <string>
 #include <vector>
 
+#include "kernels_impl.h"  // the product's kernels, launched beside the variants (-Iishmem_amd/csrc -Iinclude)
+
 #define CK(x)                                                                                      \
     do {                                                                                           \
         hipError_t e_ = (x);                                                                       \
@@ -144,26 +146,59 @@ __global__ __launch_bounds__(64) void k_unal(Args a)
     wt(uptr(a.d + wo), tid * 16u, acc);
 }
 
-// 256-thread workgroups (4 KiB of dest): aligned loads, neighbour through LDS, lane 255 loads.
-template <int NS>
-__global__ __launch_bounds__(256) void k_lds(Args a)
+// BS-thread workgroups (BS * 16 B of dest): aligned loads, neighbour through LDS, the last lane
+// loads the next vector itself (one extra line per BS * 16 B).
+template <int NS, int BS, bool XCD>
+__global__ __launch_bounds__(BS) void k_lds(Args a)
 {
-    __shared__ u32x4 sh[NS][256];
+    __shared__ u32x4 sh[NS][BS];
     const uint32_t tid = threadIdx.x;
-    const uint64_t i0 = (uint64_t) blockIdx.x * 256;
+    const uint64_t i0 = lblock(blockIdx.x, gridDim.x, XCD) * BS;
+    if (i0 >= a.nitems) return;
     const uint64_t wo = i0 * 16;
     u32x4 A[NS], B[NS];
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
         const auto r = rsrc(uptr(a.s[j] + wo));
         A[j] = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, kNT);
-        if (tid == 255) B[j] = __builtin_amdgcn_raw_buffer_load_b128(r, 256 * 16u, 0, kNT);
+        if (tid == BS - 1) B[j] = __builtin_amdgcn_raw_buffer_load_b128(r, BS * 16u, 0, kNT);
         sh[j][tid] = A[j];
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NS; ++j)
-        if (tid < 255) B[j] = sh[j][tid + 1];
+        if (tid < BS - 1) B[j] = sh[j][tid + 1];
+    u32x4 acc = funnel16(A[0], B[0], a.k);
+    if (NS == 2) acc = addv(acc, funnel16(A[1], B[1], a.k));
+    if (i0 + tid < a.nitems) wt(uptr(a.d + wo), tid * 16u, acc);
+}
+
+// As k_lds, but only the wave boundaries go through LDS: within a wave the neighbour comes by a
+// DPP wave shift, lane 63 of wave w takes lane 0 of wave w + 1 from LDS.
+template <int NS, int BS>
+__global__ __launch_bounds__(BS) void k_ldsdpp(Args a)
+{
+    __shared__ u32x4 sh[NS][BS / 64 + 1];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t i0 = (uint64_t) blockIdx.x * BS;
+    if (i0 >= a.nitems) return;
+    const uint64_t wo = i0 * 16;
+    u32x4 A[NS], B[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const auto r = rsrc(uptr(a.s[j] + wo));
+        A[j] = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, kNT);
+        if (tid == BS - 1) sh[j][BS / 64] = __builtin_amdgcn_raw_buffer_load_b128(r, BS * 16u, 0, kNT);
+        if (lane == 0) sh[j][w] = A[j];
+        B[j].x = __builtin_amdgcn_update_dpp(0u, A[j].x, 0x130, 0xF, 0xF, false);
+        B[j].y = __builtin_amdgcn_update_dpp(0u, A[j].y, 0x130, 0xF, 0xF, false);
+        B[j].z = __builtin_amdgcn_update_dpp(0u, A[j].z, 0x130, 0xF, 0xF, false);
+        B[j].w = __builtin_amdgcn_update_dpp(0u, A[j].w, 0x130, 0xF, 0xF, false);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+        if (lane == 63) B[j] = sh[j][w + 1];
     u32x4 acc = funnel16(A[0], B[0], a.k);
     if (NS == 2) acc = addv(acc, funnel16(A[1], B[1], a.k));
     if (i0 + tid < a.nitems) wt(uptr(a.d + wo), tid * 16u, acc);
@@ -214,6 +249,22 @@ __global__ __launch_bounds__(64) void k_dpp2(Args a)
     if (i0 + 64 + tid < a.nitems) wt(db, tid * 16u + 1024u, acc[1]);
 }
 
+// The product's kernels with FaninArgs built as runtime.cpp plan_fanin builds them.
+static ishmemi::FaninArgs prod_args(const Args &a, int ns, bool aligned)
+{
+    ishmemi::FaninArgs f{};
+    f.nsrc = ns;
+    for (int j = 0; j < ns; ++j) f.src[j] = a.s[j] + a.k;
+    f.dst = a.d;
+    f.head = 0;
+    f.nitems = a.nitems;
+    f.tail = 0;
+    f.realign = aligned ? 0 : 1;
+    for (int j = 0; j < ns; ++j) f.shift[j] = a.k;
+    f.total = a.nitems * 16;
+    return f;
+}
+
 struct Variant {
     std::string name;
     int ns;
@@ -221,7 +272,86 @@ struct Variant {
     uint64_t per_wg;     // items per workgroup
     bool aligned;        // k = 0
     void (*kern)(Args);
+    int prod = 0;  // 1: product aligned fanin_kernel, 2: product fanin_realign_kernel
 };
+
+// Product-kernel variants (what makes fanin_realign_kernel slower than k_ldsdpp?):
+//   V bit 0: descriptor bound 0x7FFFFFFF instead of the source's end;  bit 1: one shift (shift[0])
+//   for both sources;  bit 2: funnel by dynamic register indexing instead of the switch;
+//   bit 3: one-shot (early return) instead of the grid-stride loop.
+[[maybe_unused]] __device__ __forceinline__ u32x4 funnel_idx(const u32x4 &A, const u32x4 &B, uint32_t k)
+{
+    const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    const uint32_t q = __builtin_amdgcn_readfirstlane(k >> 2), r = k & 3;
+    return u32x4{__builtin_amdgcn_alignbyte(W[q + 1], W[q], r), __builtin_amdgcn_alignbyte(W[q + 2], W[q + 1], r),
+                 __builtin_amdgcn_alignbyte(W[q + 3], W[q + 2], r), __builtin_amdgcn_alignbyte(W[q + 4], W[q + 3], r)};
+}
+
+// var24 of the round-5 ablation: the product structure with each source loaded, its edge vector
+// stored to LDS and published before the next source is issued, one-shot (this is the order the
+// product kernel now uses; the ablation's other variants are recorded in profiles/r05/realign/).
+template <int NS, int V>
+__global__ __launch_bounds__(ishmemi::kRealignBlock) void k_prodvar(ishmemi::FaninArgs a)
+{
+    using namespace ishmemi;
+    __shared__ u32x4 edge[NS][kRealignWaves];
+    __shared__ u32x4 edge2[NS][1];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i0 = (uint64_t) blockIdx.x * kRealignBlock;
+    if (i0 >= a.nitems) return;
+    const uint64_t wo = i0 * 16;
+    u32x4 A[NS], B[NS];
+    uint32_t sh[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        sh[j] = (V & 2) ? a.shift[0] : a.shift[j];
+        const char *sb = uniform_ptr(a.src[j] + (wo - sh[j]));
+        const auto r = make_rsrc(sb);
+        A[j] = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, kNonTemporal);
+        if (tid == kRealignBlock - 1) edge2[j][0] = __builtin_amdgcn_raw_buffer_load_b128(r, kRealignBlock * 16u, 0, kNonTemporal);
+        if ((tid & 63) == 0) edge[j][tid >> 6] = A[j];
+        B[j] = wave_next(A[j]);
+    }
+    __syncthreads();
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        if ((tid & 63) == 63) B[j] = tid == kRealignBlock - 1 ? edge2[j][0] : edge[j][(tid >> 6) + 1];
+        acc = acc + ishmemi::funnel16(A[j], B[j], sh[j]);
+    }
+    if (i0 + tid < a.nitems) wt_store(make_rsrc(uniform_ptr(a.dst + wo)), tid * 16u, acc);
+}
+
+static void launch(const Variant &v, const Args &a, hipStream_t st)
+{
+    const unsigned g = (unsigned) ((a.nitems + v.per_wg - 1) / v.per_wg);
+    if (v.prod == 0) {
+        hipLaunchKernelGGL(v.kern, dim3(g), dim3(v.block), 0, st, a);
+        return;
+    }
+    const ishmemi::FaninArgs f = prod_args(a, v.ns, v.prod == 1);
+    using namespace ishmemi;
+    if (v.prod >= 16) {
+        const int V = v.prod - 16;
+        auto go = [&](auto k1, auto k2) {
+            if (v.ns == 1) hipLaunchKernelGGL(k1, dim3(g), dim3(v.block), 0, st, f);
+            else hipLaunchKernelGGL(k2, dim3(g), dim3(v.block), 0, st, f);
+        };
+        switch (V) {
+            case 24: go(k_prodvar<1, 24>, k_prodvar<2, 24>); break;
+            case 26: go(k_prodvar<1, 26>, k_prodvar<2, 26>); break;
+            default: break;
+        }
+        return;
+    }
+    if (v.prod == 1) {
+        if (v.ns == 1) hipLaunchKernelGGL((fanin_kernel<uint32_t, ISHMEMI_OP_SUM, true, 1>), dim3(g), dim3(v.block), 0, st, f);
+        else hipLaunchKernelGGL((fanin_kernel<uint32_t, ISHMEMI_OP_SUM, true, 2>), dim3(g), dim3(v.block), 0, st, f);
+    } else {
+        if (v.ns == 1) hipLaunchKernelGGL((fanin_realign_kernel<uint32_t, ISHMEMI_OP_SUM, 1>), dim3(g), dim3(v.block), 0, st, f);
+        else hipLaunchKernelGGL((fanin_realign_kernel<uint32_t, ISHMEMI_OP_SUM, 2>), dim3(g), dim3(v.block), 0, st, f);
+    }
+}
 
 int main(int argc, char **argv)
 {
@@ -241,27 +371,14 @@ int main(int argc, char **argv)
     CK(hipMemcpy(s0, h.data(), bytes + 4096, hipMemcpyHostToDevice));
     CK(hipMemcpy(s1, h1.data(), bytes + 4096, hipMemcpyHostToDevice));
     std::vector<Variant> vs = {
-        {"copy aligned", 1, 64, 64, true, k_aligned<1>},
-        {"copy shfl", 1, 64, 64, false, k_realign<1, X_SHFL, false>},
-        {"copy dpp", 1, 64, 64, false, k_realign<1, X_DPP, false>},
-        {"copy two-loads", 1, 64, 64, false, k_realign<1, X_TWO, false>},
-        {"copy shfl xcd8", 1, 64, 64, false, k_realign<1, X_SHFL, true>},
-        {"copy dpp xcd8", 1, 64, 64, false, k_realign<1, X_DPP, true>},
-        {"copy unaligned buf", 1, 64, 64, false, k_unal<1, true, false>},
-        {"copy unaligned glb", 1, 64, 64, false, k_unal<1, false, false>},
-        {"copy unaligned buf xcd8", 1, 64, 64, false, k_unal<1, true, true>},
-        {"copy lds256", 1, 256, 256, false, k_lds<1>},
-        {"copy dpp2", 1, 64, 128, false, k_dpp2<1>},
-        {"a+b aligned", 2, 64, 64, true, k_aligned<2>},
-        {"a+b shfl", 2, 64, 64, false, k_realign<2, X_SHFL, false>},
-        {"a+b dpp", 2, 64, 64, false, k_realign<2, X_DPP, false>},
-        {"a+b two-loads", 2, 64, 64, false, k_realign<2, X_TWO, false>},
-        {"a+b dpp xcd8", 2, 64, 64, false, k_realign<2, X_DPP, true>},
-        {"a+b unaligned buf", 2, 64, 64, false, k_unal<2, true, false>},
-        {"a+b unaligned glb", 2, 64, 64, false, k_unal<2, false, false>},
-        {"a+b unaligned buf xcd8", 2, 64, 64, false, k_unal<2, true, true>},
-        {"a+b lds256", 2, 256, 256, false, k_lds<2>},
-        {"a+b dpp2", 2, 64, 128, false, k_dpp2<2>},
+        {"copy aligned", 1, 64, 64, true, nullptr, 1},
+        {"copy ldsdpp512", 1, 512, 512, false, k_ldsdpp<1, 512>},
+        {"copy var24 serial oneshot", 1, 512, 512, false, nullptr, 16 + 24},
+        {"copy product realign", 1, 512, 512, false, nullptr, 2},
+        {"a+b aligned", 2, 64, 64, true, nullptr, 1},
+        {"a+b ldsdpp512", 2, 512, 512, false, k_ldsdpp<2, 512>},
+        {"a+b var24 serial oneshot", 2, 512, 512, false, nullptr, 16 + 24},
+        {"a+b product realign", 2, 512, 512, false, nullptr, 2},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
@@ -274,8 +391,7 @@ int main(int argc, char **argv)
     for (size_t v = 0; v < vs.size(); ++v) {  // correctness, once per variant
         Args a{{s0, s1}, d, n, vs[v].aligned ? 0u : kshift, bytes};
         CK(hipMemset(d, 0, bytes));
-        const unsigned g = (unsigned) ((n + vs[v].per_wg - 1) / vs[v].per_wg);
-        hipLaunchKernelGGL(vs[v].kern, dim3(g), dim3(vs[v].block), 0, st, a);
+        launch(vs[v], a, st);
         CK(hipStreamSynchronize(st));
         CK(hipMemcpy(got.data(), d, bytes, hipMemcpyDeviceToHost));
         const uint32_t k = a.k;
@@ -292,10 +408,9 @@ int main(int argc, char **argv)
     for (int r = 0; r < rounds; ++r) {
         for (size_t v = 0; v < vs.size(); ++v) {
             Args a{{s0, s1}, d, n, vs[v].aligned ? 0u : kshift, bytes};
-            const unsigned g = (unsigned) ((n + vs[v].per_wg - 1) / vs[v].per_wg);
-            hipLaunchKernelGGL(vs[v].kern, dim3(g), dim3(vs[v].block), 0, st, a);
+            launch(vs[v], a, st);
             CK(hipEventRecord(e0, st));
-            for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(vs[v].kern, dim3(g), dim3(vs[v].block), 0, st, a);
+            for (int i = 0; i < iters; ++i) launch(vs[v], a, st);
             CK(hipEventRecord(e1, st));
             CK(hipEventSynchronize(e1));
             float t;
