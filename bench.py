@@ -293,6 +293,9 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
                between barriers) and on the persistent kernel (the phased threshold, 4 MiB);
       phased_peer_nt - 64 MiB and the payload on the phased path with nontemporal peer loads
                (the collectives issue sc0 sc1 ones; the tripwire_peer_nt leg checks coherence);
+      barrier_kernel / barrier_stream - the phased path at 1 / 4 / 16 MiB and the payload with its
+               three team barriers as the one-workgroup barrier kernel (default) or as stream
+               memory operations (ISHMEM_BARRIER_KIND=stream: the command processor waits);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
       ll    - 4 / 16 / 64 KiB with the one-hop granule path on (default) and off."""
 
@@ -339,6 +342,10 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     for nb in sorted({64 << 20, B}):
         if nb <= B:  # the phased grids' peer loads nontemporal instead of sc0 sc1 (measurement only)
             run("phased_peer_nt", "phased_peer_nt", 1, nb, 5 if nb == B else 20, also={"phased_min_bytes": 0})
+    for nb in sorted({1 << 20, 4 << 20, 16 << 20, B}):
+        if nb <= B:  # set alike on every rank (the two kinds use different flag rows)
+            for kind, case in ((0, "barrier_kernel"), (1, "barrier_stream")):
+                run(case, "barrier_kind", kind, nb, 5 if nb == B else 20, also={"phased_min_bytes": 0})
     if world == 2:
         run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
         run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)

@@ -237,6 +237,7 @@ struct PeRecord {
     int64_t max_blocks, ll_max_bytes, oneshot_p2, phased_min;
     uint64_t staging_bytes;
     int64_t staging_slots;
+    int32_t barrier_kind, pad_;
     hipIpcMemHandle_t heap_handle;
     hipIpcMemHandle_t flags_handle;
 };
@@ -296,6 +297,13 @@ struct State {
     // Measurement only (set_param "phased_peer_nt"): the phased grids load peers' bytes
     // nontemporal instead of sc0 sc1 (kernels.h PhaseArgs::peer_nt).  Must be set alike on every PE.
     int phased_peer_nt = 0;
+    // Team barriers of the phased paths and ishmem_team_sync: 0 = the one-workgroup barrier
+    // kernel (team_sync_kernel), 1 = stream memory operations (ISHMEM_BARRIER_KIND=stream: the
+    // command processor waits, no workgroup is held; team_barrier).  Agreed at init; sb_epoch is
+    // the stream barrier's per-team epoch, counted on the host (every member calls the same
+    // collectives of a team in the same order) and reset with the team's flag block.
+    int barrier_kind = 0;
+    uint32_t sb_epoch[kMaxTeams] = {};
     hipEvent_t ev_in[kMaxStagingSlots] = {}, ev_red[kMaxStagingSlots] = {}, ev_out[kMaxStagingSlots] = {};
 
     Team teams[kMaxTeams];
@@ -602,6 +610,36 @@ bool capturing(hipStream_t st)
     return cs != hipStreamCaptureStatusNone;
 }
 
+// Team barrier on `st`, stream ordered (everything before it on the stream has completed on this
+// PE, and on every member, when the stream passes it).  barrier_kind 0: team_sync_kernel, one
+// workgroup polling the flag row (kPhaseSync, 0) with a bounded spin (*ret on timeout).
+// barrier_kind 1 (ISHMEM_BARRIER_KIND=stream): stream memory operations —
+// hipStreamWriteValue32 of the team's next epoch into this PE's slot of row (kPhaseSync, 1) on
+// every peer (IPC-mapped flag blocks), then hipStreamWaitValue32 (>=) on the p - 1 peer slots of
+// its own row: the command processor waits, no workgroup is resident.  It has no timeout (a
+// missing member stalls the stream, not a bounded spin).  Measured on one GPU (tools/
+// streamop_probe.hip, two streams of one process): a two-party stream-op barrier 9.6 us against
+// 5.7 us for the barrier kernel; which is cheaper over xGMI between processes is for the node run
+// (the N > 1 bench's xgmi_tuning leg times both).  A captured stream (hipGraph) keeps the kernel
+// barrier: a captured write would replay a stale epoch.  Every PE must take the same kind (agreed
+// at init); PEs that differ in capturing one call would use different rows.
+int team_barrier(State &s, int team, const ReduceArgs &a, hipStream_t st)
+{
+    if (s.barrier_kind != 1 || a.p <= 1 || capturing(st)) {
+        HIP_TRY(launch_team_sync(a, st));
+        return 0;
+    }
+    uint32_t e = ++s.sb_epoch[team];
+    if (e == 0) e = s.sb_epoch[team] = 1;  // 2^32 barriers of one team: the flags restart at 0
+    const size_t row = ((size_t) kPhaseSync * kMaxBlocks + 1) * kMaxPes;
+    for (int j = 0; j < a.p; ++j)
+        if (j != a.me) HIP_TRY(hipStreamWriteValue32(st, a.peer_flags[j] + row + a.me, e, 0));
+    for (int j = 0; j < a.p; ++j)
+        if (j != a.me) HIP_TRY(hipStreamWaitValue32(st, a.my_flags + row + j, e, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    return 0;
+}
+
+
 // Work captured into a hipGraph runs when the graph is launched: ordering it against other
 // collectives is the caller's (launch order), so captured calls neither wait nor mark.
 int order_stream(State &s, hipStream_t st)
@@ -734,15 +772,15 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
             return 0;
         };
         if (mark(0)) return 1;
-        HIP_TRY(launch_team_sync(a, st));
+        if (team_barrier(s, team, a, st)) return 1;
         if (mark(1)) return 1;
         HIP_TRY(launch_rs_phase(op, dt, ph, st));
         if (mark(2)) return 1;
-        HIP_TRY(launch_team_sync(a, st));
+        if (team_barrier(s, team, a, st)) return 1;
         if (mark(3)) return 1;
         HIP_TRY(launch_ag_phase(ph, st));
         if (mark(4)) return 1;
-        HIP_TRY(launch_team_sync(a, st));
+        if (team_barrier(s, team, a, st)) return 1;
         if (mark(5)) return 1;
         s.phase_recorded = s.phase_recorded || ev;
         return 0;
@@ -960,9 +998,9 @@ int collect_launch(State &s, int team, void *dst, const void *src, const uint64_
         ReduceArgs r;
         if (team_args(s, team, r, why)) return fail("collect: " + why);
         r.ret = ret;
-        HIP_TRY(launch_team_sync(r, st));
+        if (team_barrier(s, team, r, st)) return 1;
         HIP_TRY(launch_collect_phase(a, st));
-        HIP_TRY(launch_team_sync(r, st));
+        if (team_barrier(s, team, r, st)) return 1;
         return 0;
     }
     const uint64_t items = maxb / a.unit, tile = (uint64_t) kBlock * kUnroll;
@@ -1197,9 +1235,9 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
             if (team_args(s, team, r, why)) return fail("scan: " + why);
             r.ret = ret;
             const bool vec = ((d0 | s0) & 15) == 0;
-            HIP_TRY(launch_team_sync(r, st));
+            if (team_barrier(s, team, r, st)) return 1;
             HIP_TRY(launch_scan_direct(dt, a, vec, st));
-            HIP_TRY(launch_team_sync(r, st));
+            if (team_barrier(s, team, r, st)) return 1;
             if (mark_stream(s, st)) return 1;
             if (blocking) {
                 HIP_TRY(hipStreamSynchronize(st));
@@ -1231,11 +1269,11 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
                 ReduceArgs r;
                 if (team_args(s, team, r, why)) return fail("scan: " + why);
                 r.ret = ret;
-                HIP_TRY(launch_team_sync(r, st));
+                if (team_barrier(s, team, r, st)) return 1;
                 HIP_TRY(launch_scan_phase(dt, a, vec, 1, st));
-                HIP_TRY(launch_team_sync(r, st));
+                if (team_barrier(s, team, r, st)) return 1;
                 HIP_TRY(launch_scan_phase(dt, a, vec, 2, st));
-                HIP_TRY(launch_team_sync(r, st));
+                if (team_barrier(s, team, r, st)) return 1;
                 continue;
             }
             const uint64_t tile = (uint64_t) kBlock * 2 * (vec ? 16 / es : 1);
@@ -1262,7 +1300,7 @@ int team_sync_locked(State &s, int team, hipStream_t st, int *ret)
     std::string why;
     if (team_args(s, team, a, why)) return fail("team_sync: " + why);
     a.ret = ret;
-    HIP_TRY(launch_team_sync(a, st));
+    if (team_barrier(s, team, a, st)) return 1;
     return 0;
 }
 
@@ -1459,6 +1497,13 @@ int init_impl(int pe, int npes, int device, const std::string &key)
 #endif
     const bool ep_uncached = env_ll("ISHMEM_EP_UNCACHED", 0) != 0;
     s.phased_peer_nt = env_ll("ISHMEM_PHASED_PEER_NT", 0) != 0;
+    s.barrier_kind = 0;
+    for (int t = 0; t < kMaxTeams; ++t) s.sb_epoch[t] = 0;
+    if (const char *bk = getenv("ISHMEM_BARRIER_KIND"); bk && *bk) {
+        if (strcasecmp(bk, "stream") == 0) s.barrier_kind = 1;
+        else if (strcasecmp(bk, "kernel") != 0 && g_env_error.empty())
+            g_env_error = std::string("ISHMEM_BARRIER_KIND='") + bk + "' is not 'kernel' or 'stream'";
+    }
     if (!g_env_error.empty()) {
         const std::string e = g_env_error;
         g_env_error.clear();
@@ -1520,6 +1565,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.phased_min = s.phased_min;
         mine.staging_bytes = s.staging_bytes;
         mine.staging_slots = s.staging_slots;
+        mine.barrier_kind = s.barrier_kind;
         if (hipDeviceGetPCIBusId(mine.pci_bus, sizeof(mine.pci_bus), s.device) != hipSuccess) {
             (void) hipGetLastError();
             snprintf(mine.pci_bus, sizeof(mine.pci_bus), "dev%d", s.device);
@@ -1555,6 +1601,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             if (j == pe) continue;
             if (all[j].heap_size != s.heap_size)
                 return fail("init: ISHMEM_SYMMETRIC_SIZE differs between PEs");
+            if (all[j].barrier_kind != s.barrier_kind)
+                return fail("init: ISHMEM_BARRIER_KIND differs between PEs (the barrier kinds use different flag rows)");
             if (all[j].device != s.device) {
                 // The kernels load peers' memory directly over xGMI: without peer access those
                 // loads would fault the GPU, so refuse to initialise instead.
@@ -2138,6 +2186,7 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
         // from this team (every member of this one has the slot reserved, so the AND-reduced
         // mask of any parent containing one of them excludes it): flag blocks never collide.
         if (t.my_idx >= 0) s.teams[slot] = t;
+        s.sb_epoch[slot] = 0;
         // Fresh flag block: zero it locally, then the parent sync below orders the zeroing
         // before any member's first barrier on the new team.
         if (hipMemset(team_flags(s.flags, slot), 0, kTeamFlagBytes) != hipSuccess ||
@@ -2625,6 +2674,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "ll_max_bytes") s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes, std::max<long long>(0, value));
     else if (n == "debug") s.debug = (int) value;
     else if (n == "phased_peer_nt") s.phased_peer_nt = value != 0;
+    else if (n == "barrier_kind") s.barrier_kind = value != 0 ? 1 : 0;  // measurement: set alike on every PE
     else if (n == "trace_buffer") s.trace = (uint64_t *) (uintptr_t) value;
     else if (n == "phase_events") {
         if (value && !s.phase_ev[0])
@@ -2649,6 +2699,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "ll_max_bytes") return s.ll_max_bytes;
     if (n == "debug") return s.debug;
     if (n == "phased_peer_nt") return s.phased_peer_nt;
+    if (n == "barrier_kind") return s.barrier_kind;
     if (n == "flags_fine_grained") return s.flags_kind != kFlagsCoarse ? 1 : 0;
     if (n == "flags_kind") return s.flags_kind;
     if (n == "staging_bytes") return (long long) s.staging_bytes;

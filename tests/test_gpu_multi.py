@@ -175,6 +175,21 @@ def test_phased_reduce_scatter_allgather_path(npes):
             timeout=400)
 
 
+@pytest.mark.parametrize("npes", [2, 3, 8])
+def test_phased_path_with_stream_memop_barriers(npes):
+    # ISHMEM_BARRIER_KIND=stream: the phased paths' team barriers (and
+    # ishmem_team_sync) as hipStreamWriteValue32 into the peers' flag rows + hipStreamWaitValue32 on
+    # the own row, instead of the one-workgroup barrier kernel.  Forced for every heap reduce with a
+    # 16-B body: golden inputs, in place, the offset sweeps, edges, 256 MiB in full, hipGraph replay
+    # (captured calls keep the kernel barrier) and the chained-producer tripwire; plus the phased
+    # collect / scan at 2 and 3 PEs.
+    scen = ["golden", "inplace", "offsets", "offsets_large", "edge", "large", "graph", "tripwire"]
+    if npes < 8:
+        scen += ["collect", "scan"]
+    run_pes(npes, scen, env={"ISHMEM_BARRIER_KIND": "stream", "ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0,
+                             "ISHMEM_ONESHOT_P2_MAX_BYTES": 0, "ISHMEM_MAX_BLOCKS": 64}, timeout=400)
+
+
 @pytest.mark.parametrize("npes", [2, 4])
 def test_phased_path_with_nontemporal_peer_loads(npes):
     # The measurement-only mode the N > 1 bench times over xGMI (ISHMEM_PHASED_PEER_NT /
