@@ -930,9 +930,14 @@ __global__ __launch_bounds__(kFaninBlock) void fanin_kernel(FaninArgs a)
             // a + b 0.471-0.472 ms against 0.484-0.485 ms with global nt loads, 1 GiB, interleaved
             // A B x3 (profiles/r04/fanin_loads/); the copy (NS = 1) keeps global loads, which were
             // 0.7 % faster there.
+            // Source 1's load is issued once source 0's has landed: a + b 0.473 ms against 0.486 ms
+            // with both in flight (one process, interleaved, tools/realign_variants.hip "serial",
+            // profiles/r05/fanin/) — fewer interleaved request streams per wave; the realigned
+            // kernel showed the same (its LDS stores order the sources).
             const uint64_t wo = off - (uint64_t) threadIdx.x * IB;
             const uint32_t lo = (uint32_t) (threadIdx.x * IB);
             const Item x0 = bload<Item>(make_rsrc(uniform_ptr(a.src[0] + wo)), lo);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const Item x1 = bload<Item>(make_rsrc(uniform_ptr(a.src[1] + wo)), lo);
             acc = op1<T, OP>(x0, x1);
         } else if constexpr (NS == 2) {

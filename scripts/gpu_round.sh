@@ -8,7 +8,6 @@ TAG="${1:-r01}"; shift || true
 STEPS="${*:-smoke single multi bench prof}"
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
-export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd "$R"
 
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }

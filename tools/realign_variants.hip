@@ -82,6 +82,29 @@ __global__ __launch_bounds__(64) void k_aligned(Args a)
     wt(uptr(a.d + (i - threadIdx.x) * 16), threadIdx.x * 16u, x);
 }
 
+// Aligned copy / a + b shapes (round 5): BS threads per workgroup, U 16-B items per thread (all
+// loads before the stores), store cache policy SAUX (17 = sc0 sc1 write-through, 2 = nt,
+// 1 = sc0, 16 = sc1, 0 = default), buffer loads based at the workgroup's first item.
+template <int NS, int BS, int U, int SAUX, bool SERIAL = false>
+__global__ __launch_bounds__(BS) void k_al(Args a)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i0 = (uint64_t) blockIdx.x * BS * U;
+    if (i0 >= a.nitems) return;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t off = (u * BS + tid) * 16u;
+        x[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(uptr(a.s[0] + i0 * 16)), off, 0, kNT);
+        if (SERIAL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (NS == 2) x[u] = addv(x[u], __builtin_amdgcn_raw_buffer_load_b128(rsrc(uptr(a.s[1] + i0 * 16)), off, 0, kNT));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (i0 + u * BS + tid < a.nitems)
+            __builtin_amdgcn_raw_buffer_store_b128(x[u], rsrc(uptr(a.d + i0 * 16)), (u * BS + tid) * 16u, 0, SAUX);
+}
+
 // Neighbour exchange flavours for the aligned-load + funnel family.
 enum { X_SHFL = 0, X_DPP = 1, X_TWO = 2 };
 
@@ -371,13 +394,10 @@ int main(int argc, char **argv)
     CK(hipMemcpy(s0, h.data(), bytes + 4096, hipMemcpyHostToDevice));
     CK(hipMemcpy(s1, h1.data(), bytes + 4096, hipMemcpyHostToDevice));
     std::vector<Variant> vs = {
-        {"copy aligned", 1, 64, 64, true, nullptr, 1},
-        {"copy ldsdpp512", 1, 512, 512, false, k_ldsdpp<1, 512>},
-        {"copy var24 serial oneshot", 1, 512, 512, false, nullptr, 16 + 24},
-        {"copy product realign", 1, 512, 512, false, nullptr, 2},
-        {"a+b aligned", 2, 64, 64, true, nullptr, 1},
-        {"a+b ldsdpp512", 2, 512, 512, false, k_ldsdpp<2, 512>},
-        {"a+b var24 serial oneshot", 2, 512, 512, false, nullptr, 16 + 24},
+        {"copy product aligned", 1, 64, 64, true, nullptr, 1},
+        {"a+b al 64x1 sc01", 2, 64, 64, true, k_al<2, 64, 1, 17>},
+        {"a+b al 64x1 serial", 2, 64, 64, true, k_al<2, 64, 1, 17, true>},
+        {"a+b product aligned", 2, 64, 64, true, nullptr, 1},
         {"a+b product realign", 2, 512, 512, false, nullptr, 2},
     };
     hipStream_t st;
