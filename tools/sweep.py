@@ -28,6 +28,8 @@ def main() -> None:
     ap.add_argument("--blocking", action="store_true",
                     help="blocking host calls (ishmem_fcollectmem / ishmem_float_sum_inscan / ishmem_float_sum_reduce), "
                          "timed on the host clock")
+    ap.add_argument("--src-offset", type=int, default=0, help="reduce: source starts this many bytes (a multiple of 4) past its allocation")
+    ap.add_argument("--dst-offset", type=int, default=0, help="reduce: dest starts this many bytes (a multiple of 4) past its allocation")
     ap.add_argument("--emulate-share1", action="store_true",
                     help="every PE reports its own device (ISHMEM_TEST_PCI_BUS): the launch shapes of one PE per GPU")
     args = ap.parse_args()
@@ -51,14 +53,15 @@ def main() -> None:
     dev = 0 if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else local
     ish.init(rank, world, dev, key)
     nmax = (args.max_mib << 20) // 4
-    src = ish.ishmem_malloc(nmax * 4)
-    dst = ish.ishmem_malloc(nmax * 4 * (world if args.coll == "fcollect" else 1))
-    hip.upload(src, (np.arange(nmax, dtype=np.int64) % 1024).astype(np.float32) + np.float32(rank))
+    so, do = args.src_offset // 4, args.dst_offset // 4
+    src = ish.ishmem_malloc(nmax * 4 + 64)
+    dst = ish.ishmem_malloc(nmax * 4 * (world if args.coll == "fcollect" else 1) + 64)
+    hip.upload(src, (np.arange(nmax + 16, dtype=np.int64) % 1024).astype(np.float32) + np.float32(rank))
     st = hip.stream_create()
     if rank == 0:
         print(f"# coll={args.coll} graph={args.graph} blocking={args.blocking} pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
               f"ll_max_bytes={ish.get_param('ll_max_bytes')} wait_slots={ish.get_param('wait_slots')} "
-              f"device_share={ish.get_param('device_share')}")
+              f"device_share={ish.get_param('device_share')} src_offset={args.src_offset} dst_offset={args.dst_offset}")
         print("bytes,us_per_call,algbw_GiBps,ok")
     def call(n):
         if args.blocking:
@@ -71,9 +74,10 @@ def main() -> None:
             return ish.fcollect_on_stream(dst, src, n * 4, 0, st)
         if args.coll == "inscan":
             return ish.lib().ishmemi_c_scan_on_stream(0, ish.DTYPES["float"], 1, dst, src, n, None, st)
-        return ish.ishmemx_float_sum_reduce_on_stream(dst, src, n, 0, st)
+        return ish.ishmemx_float_sum_reduce_on_stream(dst + 4 * do, src + 4 * so, n, 0, st)
 
     def expect(i, n):
+        i = i + so
         base = (i % 1024).astype(np.float32)
         if args.coll == "fcollect":  # the last k elements of the dest = PE world-1's tail
             return base + np.float32(world - 1)
@@ -123,7 +127,7 @@ def main() -> None:
             us = float(t[0])
         k = min(n, 64)
         last = n * (world if args.coll == "fcollect" else 1)
-        got = hip.download(dst + (last - k) * 4, k, np.float32)
+        got = hip.download(dst + 4 * do + (last - k) * 4, k, np.float32)
         ok = bool(np.array_equal(got, expect(np.arange(n - k, n), n)))
         if rank == 0:
             print(f"{n * 4},{us:.2f},{n * 4 / 2**30 / (us * 1e-6):.2f},{int(ok)}", flush=True)
