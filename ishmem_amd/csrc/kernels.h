@@ -162,6 +162,12 @@ constexpr int kMaxFanin = 16;
 constexpr int kRealignBlock = ISHMEMI_REALIGN_BLOCK;
 constexpr int kRealignWaves = kRealignBlock / 64;
 constexpr int kRealignMaxGrid = (int) ((1ull << 31) / kRealignBlock);
+// The phased reduce-scatter's realigned kernel (rs_phase_realign_kernel): one-wave workgroups
+// measured best there (kernels_impl.h rs_realign_block), unlike the 1-PE fan-in.
+#ifndef ISHMEMI_RS_REALIGN_BLOCK
+#define ISHMEMI_RS_REALIGN_BLOCK 64
+#endif
+constexpr int kRsRealignBlock = ISHMEMI_RS_REALIGN_BLOCK;
 // Dest alignment the realigned body starts at (the head before it runs element-wise): 256 B, so
 // the workgroups' 1 KiB store blocks cover whole lines instead of sharing one with a neighbour.
 #ifndef ISHMEMI_REALIGN_PEEL

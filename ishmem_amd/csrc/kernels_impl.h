@@ -1034,7 +1034,7 @@ __device__ __forceinline__ u32x4 wave_next(const u32x4 &A)
 // two sources that order ran a + b at 0.489-0.490 ms per GiB against 0.511-0.513 ms with both
 // sources' loads issued before any wait (tools/realign_variants.hip var24 / var8, interleaved,
 // profiles/r05/realign/).
-template <int AUX>
+template <int AUX, int BS = kRealignBlock>
 __device__ __forceinline__ void realign_issue(const char *src, uint32_t shift, uint64_t total, uint64_t wo,
                                               u32x4 *edge, u32x4 &A, u32x4 &B)
 {
@@ -1043,7 +1043,7 @@ __device__ __forceinline__ void realign_issue(const char *src, uint32_t shift, u
     const uint64_t end_al = (((uint64_t) (uintptr_t) src + total + 15) & ~15ull) - (uint64_t) (uintptr_t) sb;
     const __amdgpu_buffer_rsrc_t r = make_rsrc_n(sb, end_al);
     A = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, AUX);
-    if (tid == kRealignBlock - 1) edge[kRealignWaves] = __builtin_amdgcn_raw_buffer_load_b128(r, kRealignBlock * 16u, 0, AUX);
+    if (tid == BS - 1) edge[BS / 64] = __builtin_amdgcn_raw_buffer_load_b128(r, BS * 16u, 0, AUX);
     if ((tid & 63) == 0) edge[tid >> 6] = A;
     B = wave_next(A);
 }
@@ -1224,45 +1224,62 @@ __global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
 
 // The phased reduce-scatter with every member's source on another 16-B phase than dest (the same
 // shift on every PE: the offsets are symmetric): the realigned fan-in's loads (realign_issue /
-// realign_finish, 512-thread workgroups, DPP + LDS edges) per member, members taken four at a
-// time — their loads all in flight — and folded in team order.  Round 4 ran this inside
-// rs_phase_kernel's one-wave workgroups with four shuffles and a boundary load per member per
-// 1 KiB.  In place never gets here (source == dest has no shift), so the loads past the chunk's
-// end read only bytes no member writes during the reduce-scatter.
-template <typename T, int OP>
-__global__ __launch_bounds__(kRealignBlock) void rs_phase_realign_kernel(PhaseArgs a)
+// realign_finish, DPP + LDS edges) per member in kRsRealignBlock-thread workgroups (64: the block
+// size A/B above), members taken four at a time and folded in team order.  Round 4 ran this with
+// four shuffles per member per vector.  In place never gets here (source == dest has no shift), so
+// the loads past the chunk's end read only bytes no member writes during the reduce-scatter.
+// One BS-item block of the realigned reduce-scatter (every thread; i0 workgroup-uniform):
+// members in groups of G, each member's loads issued after the previous member's LDS store has
+// waited for its own, one barrier per group plus one between groups (edge[] reuse).  2 PEs x 1 GiB
+// on one GPU, sources 4 B off dest's phase, reduce-scatter grid (`tools/sweep.py --phases`,
+// interleaved, profiles/r05/realign_multi/): 64-thread workgroups 0.546-0.547 ms, 256 0.563-0.569,
+// 512 0.559-0.594; all members' loads issued before any wait 0.609-0.617 (64) / 0.643-0.671 (512);
+// round 4's shuffle version 0.571; aligned operands 0.487-0.493.
+template <typename T, int OP, int BS, int G>
+__device__ __forceinline__ void rs_realign_block(const PhaseArgs &a, u32x4 (*edge)[BS / 64 + 1], uint64_t i0, uint64_t ce)
 {
-    constexpr int G = 4;
-    __shared__ u32x4 edge[G][kRealignWaves + 1];
     const int p = a.p, me = a.me;
     const uint32_t tid = threadIdx.x;
-    const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
-    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
-    const uint64_t hb = a.head * sizeof(T);
-    const uint64_t stride = (uint64_t) gridDim.x * kRealignBlock;
-    for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kRealignBlock; i0 < ce; i0 += stride) {
-        const uint64_t wb = hb + i0 * 16;
-        Vec<T> acc;
-        for (int g0 = 0; g0 < p; g0 += G) {
-            u32x4 A[G], B[G];
+    const uint64_t wb = a.head * sizeof(T) + i0 * 16;
+    Vec<T> acc;
+    for (int g0 = 0; g0 < p; g0 += G) {
+        if (g0) __syncthreads();  // the previous group's edge[] reads are done
+        u32x4 A[G], B[G];
 #pragma unroll
-            for (int k = 0; k < G; ++k) {
-                const int j = g0 + k;
-                if (j >= p) break;
-                if (j == me || a.peer_nt) realign_issue<kNonTemporal>(a.src[j], a.shift, a.total, wb, edge[k], A[k], B[k]);
-                else realign_issue<kSysCoherent>(a.src[j], a.shift, a.total, wb, edge[k], A[k], B[k]);
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < G; ++k) {
-                const int j = g0 + k;
-                if (j >= p) break;
-                const Vec<T> x = __builtin_bit_cast(Vec<T>, realign_finish(edge[k], A[k], B[k], a.shift));
-                acc = j == 0 ? x : op1<T, OP>(acc, x);
-            }
-            __syncthreads();
+        for (int k = 0; k < G; ++k) {
+            const int j = g0 + k;
+            if (j >= p) break;
+            if (j == me || a.peer_nt) realign_issue<kNonTemporal, BS>(a.src[j], a.shift, a.total, wb, edge[k], A[k], B[k]);
+            else realign_issue<kSysCoherent, BS>(a.src[j], a.shift, a.total, wb, edge[k], A[k], B[k]);
         }
-        if (i0 + tid < ce) wt_store(make_rsrc(uniform_ptr(a.dst + wb)), tid * 16u, acc);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int j = g0 + k;
+            if (j >= p) break;
+            const Vec<T> x = __builtin_bit_cast(Vec<T>, realign_finish(edge[k], A[k], B[k], a.shift));
+            acc = j == 0 ? x : op1<T, OP>(acc, x);
+        }
+    }
+    if (i0 + tid < ce) wt_store(make_rsrc(uniform_ptr(a.dst + wb)), tid * 16u, acc);
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kRsRealignBlock) void rs_phase_realign_kernel(PhaseArgs a)
+{
+    constexpr int BS = kRsRealignBlock, G = 4;
+    __shared__ u32x4 edge[G][BS / 64 + 1];
+    const uint64_t cs = min((uint64_t) a.me * a.items_per_chunk, a.nitems);
+    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
+    const uint64_t stride = (uint64_t) gridDim.x * BS;
+    const uint64_t first = cs + (uint64_t) blockIdx.x * BS;
+    if (cs + stride >= ce) {
+        if (first < ce) rs_realign_block<T, OP, BS, G>(a, edge, first, ce);
+    } else {
+        for (uint64_t i0 = first; i0 < ce; i0 += stride) {
+            rs_realign_block<T, OP, BS, G>(a, edge, i0, ce);
+            __syncthreads();  // edge[] is rewritten by the next pass
+        }
     }
     rs_phase_edges<T, OP>(a);
 }
@@ -1320,9 +1337,9 @@ hipError_t rs_phase_t(const PhaseArgs &a, hipStream_t s)
         hipLaunchKernelGGL(kernel, dim3(phase_grid(kernel, len)), dim3(kFaninBlock), 0, s, a);
     };
     if (a.shift) {
-        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((len + kRealignBlock - 1) / kRealignBlock,
-                                                                    (uint64_t) kRealignMaxGrid));
-        hipLaunchKernelGGL((rs_phase_realign_kernel<T, OP>), dim3((unsigned) g), dim3(kRealignBlock), 0, s, a);
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((len + kRsRealignBlock - 1) / kRsRealignBlock,
+                                                                    (1ull << 31) / kRsRealignBlock));
+        hipLaunchKernelGGL((rs_phase_realign_kernel<T, OP>), dim3((unsigned) g), dim3(kRsRealignBlock), 0, s, a);
     } else if (a.p == 2) go(rs_phase_kernel<T, OP, 2>);
     else if (a.p == 4) go(rs_phase_kernel<T, OP, 4>);
     else if (a.p == 8) go(rs_phase_kernel<T, OP, 8>);

@@ -2316,12 +2316,15 @@ int ishmemi_c_resync(void)
     if (!s.initialized) return fail("resync: not initialized");
     HIP_TRY(hipDeviceSynchronize());
     struct Epochs {
-        uint32_t host[kMaxTeams], dev[kMaxTeams];
+        uint32_t host[kMaxTeams], dev[kMaxTeams], sb[kMaxTeams];  // sb: stream barriers (team_barrier)
     } mine{}, all[kMaxPes];
     std::vector<uint32_t> words((size_t) kMaxTeams * kEpTeamWords);
     HIP_TRY(hipMemcpy(words.data(), s.kern_ep, words.size() * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(mine.dev, s.dev_epochs, sizeof(mine.dev), hipMemcpyDeviceToHost));
-    for (int t = 0; t < kMaxTeams; ++t) mine.host[t] = words[(size_t) t * kEpTeamWords + kEpEpoch];
+    for (int t = 0; t < kMaxTeams; ++t) {
+        mine.host[t] = words[(size_t) t * kEpTeamWords + kEpEpoch];
+        mine.sb[t] = s.sb_epoch[t];
+    }
     if (s.npes > 1) {
         std::string err;
         if (s.boot.allgather(&mine, all, sizeof(Epochs), err)) return fail("resync: " + err);
@@ -2330,11 +2333,13 @@ int ishmemi_c_resync(void)
     }
     auto newest = [](uint32_t a, uint32_t b) { return (int32_t) (b - a) > 0 ? b : a; };
     for (int t = 0; t < kMaxTeams; ++t) {
-        uint32_t h = all[0].host[t], d = all[0].dev[t];
+        uint32_t h = all[0].host[t], d = all[0].dev[t], sb = all[0].sb[t];
         for (int j = 1; j < s.npes; ++j) {
             h = newest(h, all[j].host[t]);
             d = newest(d, all[j].dev[t]);
+            sb = newest(sb, all[j].sb[t]);
         }
+        s.sb_epoch[t] = sb;
         uint32_t *w = words.data() + (size_t) t * kEpTeamWords;
         for (int k = 0; k < kEpTeamWords; ++k) w[k] = 0;
         w[kEpEpoch] = h;

@@ -30,6 +30,8 @@ def main() -> None:
                          "timed on the host clock")
     ap.add_argument("--src-offset", type=int, default=0, help="reduce: source starts this many bytes (a multiple of 4) past its allocation")
     ap.add_argument("--dst-offset", type=int, default=0, help="reduce: dest starts this many bytes (a multiple of 4) past its allocation")
+    ap.add_argument("--phases", action="store_true", help="reduce: after the sweep, one call of the largest size with "
+                    "HIP events between the phased path's five launches (rank 0's ms)")
     ap.add_argument("--emulate-share1", action="store_true",
                     help="every PE reports its own device (ISHMEM_TEST_PCI_BUS): the launch shapes of one PE per GPU")
     args = ap.parse_args()
@@ -132,6 +134,21 @@ def main() -> None:
         if rank == 0:
             print(f"{n * 4},{us:.2f},{n * 4 / 2**30 / (us * 1e-6):.2f},{int(ok)}", flush=True)
         n *= args.factor
+    if args.phases and args.coll == "reduce":
+        import ctypes
+        n = n // args.factor
+        ish.set_param("phase_events", 1)
+        for _ in range(2):
+            call(n)
+            hip.stream_synchronize(st)
+            if dist is not None:
+                dist.barrier()
+        ms = (ctypes.c_float * 5)()
+        r = ish.lib().ishmemi_c_phase_times(ms)
+        ish.set_param("phase_events", 0)
+        if rank == 0:
+            print(f"# phases bytes={n * 4} rc={r} " + " ".join(f"{k}={v:.4f}" for k, v in zip(
+                ["start", "rs", "mid", "ag", "end"], list(ms))), flush=True)
     ish.ishmem_finalize()
 
 
