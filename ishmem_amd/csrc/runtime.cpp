@@ -1840,7 +1840,7 @@ LaunchInfo launch_info()
     if (env_str("ISHMEM_PE")) {
         li.launcher = "ishmem";
         li.pe = num("ISHMEM_PE", 0);
-        li.npes = num("ISHMEM_NPES", num("WORLD_SIZE", 1));
+        li.npes = env_str("ISHMEM_NPES") ? num("ISHMEM_NPES", 1) : num("WORLD_SIZE", 1);
         li.local = num("LOCAL_RANK", 0);
     } else if (env_str("RANK")) {
         li.launcher = "torchrun";

@@ -980,10 +980,13 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 n = max(1, min(n, nmax))
                 o = int(rng.integers(0, 4))
                 inplace = bool(rng.random() < 0.25)
+                # Source offset drawn separately (round 5): sources on another 16-B phase than dest
+                # take the realigned reduce-scatter (phased sizes) or the element-granular path.
+                so = o if rng.random() < 0.5 else int(rng.integers(0, 4))
                 th, members = teams[int(rng.integers(len(teams)))]
                 occupier = int(rng.integers(npes)) if rng.random() < 0.2 else -1
                 cap = [int(rng.choice([16, 64, 256, 1024])) for _ in range(npes)]
-                tag = (f"stress k={k} op={ONAMES[op]} dt={NAMES[dt]} n={n} o={o} inplace={inplace} "
+                tag = (f"stress k={k} op={ONAMES[op]} dt={NAMES[dt]} n={n} o={o} so={so} inplace={inplace} "
                        f"team={members} occ={occupier} cap={cap[pe]}")
                 ish.set_param("max_blocks", cap[pe])
                 lo, hi = (0.5, 2.0) if op == OPS["prod"] else (-1.0, 1.0)
@@ -992,7 +995,7 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 hip.memset(D, 0xA5, (nmax + 2 * pad) * 8)
                 hip.synchronize()
                 dbase = D + pad * 8 + o * es
-                sbase = dbase if inplace else S + pad * 8 + o * es
+                sbase = dbase if inplace else S + pad * 8 + so * es
                 if pe in members:
                     hip.upload(sbase, ins[members.index(pe)])
                 ish.ishmem_barrier_all()
