@@ -282,6 +282,34 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max):
     return out
 
 
+def stream_barrier_probe(ish, hip, dist, stream, limit_s: float = 20.0) -> bool:
+    """One stream-memory-op team barrier (ISHMEM_BARRIER_KIND=stream) on every rank before the
+    tuning leg times them: that barrier has no timeout, and it has never run between two GPUs, so a
+    barrier that does not complete within limit_s on some rank is released on every rank
+    (set_param "stream_barrier_release" stores the awaited epoch into the rank's own wait row) and
+    the rows are skipped — the leg must not hang the measured line."""
+    import time as _t
+    old = ish.get_param("barrier_kind")
+    ish.set_param("barrier_kind", 1)
+    try:
+        if ish.team_sync_on_stream(0, None, stream) != 0:
+            done = False
+        else:
+            t0 = _t.monotonic()
+            done = hip.stream_query(stream)
+            while not done and _t.monotonic() - t0 < limit_s:
+                _t.sleep(0.01)
+                done = hip.stream_query(stream)
+        stuck = max_over_ranks(dist, [0.0 if done else 1.0])[0] > 0
+        if stuck:
+            ish.set_param("stream_barrier_release", 0)
+            hip.stream_synchronize(stream)
+            dist.barrier()
+        return not stuck
+    finally:
+        ish.set_param("barrier_kind", old)
+
+
 def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     """N>1: the f32 sum again under other launch shapes, set alike on every rank, so the driver's
     multi-GPU run records how the xGMI path responds (data for choosing the defaults; one
@@ -342,10 +370,14 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     for nb in sorted({64 << 20, B}):
         if nb <= B:  # the phased grids' peer loads nontemporal instead of sc0 sc1 (measurement only)
             run("phased_peer_nt", "phased_peer_nt", 1, nb, 5 if nb == B else 20, also={"phased_min_bytes": 0})
-    for nb in sorted({1 << 20, 4 << 20, 16 << 20, B}):
-        if nb <= B:  # set alike on every rank (the two kinds use different flag rows)
-            for kind, case in ((0, "barrier_kernel"), (1, "barrier_stream")):
-                run(case, "barrier_kind", kind, nb, 5 if nb == B else 20, also={"phased_min_bytes": 0})
+    if stream_barrier_probe(ish, hip, dist, stream):
+        for nb in sorted({1 << 20, 4 << 20, 16 << 20, B}):
+            if nb <= B:  # set alike on every rank (the two kinds use different flag rows)
+                for kind, case in ((0, "barrier_kernel"), (1, "barrier_stream")):
+                    run(case, "barrier_kind", kind, nb, 5 if nb == B else 20, also={"phased_min_bytes": 0})
+    else:
+        out.append({"case": "barrier_stream", "error": "a probe stream barrier did not complete within 20 s on "
+                                                        "some rank; released (set_param stream_barrier_release)"})
     if world == 2:
         run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
         run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)

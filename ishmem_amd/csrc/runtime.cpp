@@ -2680,6 +2680,22 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "debug") s.debug = (int) value;
     else if (n == "phased_peer_nt") s.phased_peer_nt = value != 0;
     else if (n == "barrier_kind") s.barrier_kind = value != 0 ? 1 : 0;  // measurement: set alike on every PE
+    else if (n == "stream_barrier_release") {
+        // Escape hatch of the stream barrier, which has no timeout (team_barrier): store the team's
+        // latest stream-barrier epoch into every slot of this PE's own wait row, so a stream stuck
+        // in hipStreamWaitValue32 for a member that never wrote moves on.  For a caller that saw
+        // a stream barrier not complete (bench.py's probe); the barrier's result is then void.
+        const int team = (int) value;
+        if (team < 0 || team >= kMaxTeams || !s.teams[team].valid) return fail("set_param: stream_barrier_release: invalid team");
+        const size_t row = ((size_t) kPhaseSync * kMaxBlocks + 1) * kMaxPes;
+        hipStream_t rs = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking));
+        hipError_t e = hipMemsetD32Async((hipDeviceptr_t) (team_flags(s.flags, team) + row), (int) s.sb_epoch[team],
+                                         kMaxPes, rs);
+        if (e == hipSuccess) e = hipStreamSynchronize(rs);
+        (void) hipStreamDestroy(rs);
+        if (e != hipSuccess) return hipfail("stream_barrier_release", e);
+    }
     else if (n == "trace_buffer") s.trace = (uint64_t *) (uintptr_t) value;
     else if (n == "phase_events") {
         if (value && !s.phase_ev[0])

@@ -109,6 +109,17 @@ def stream_destroy(s: int) -> None:
     _check(lib().hipStreamDestroy(ctypes.c_void_p(s)), "hipStreamDestroy")
 
 
+def stream_query(s: int) -> bool:
+    """True when every operation on stream s has completed (hipStreamQuery)."""
+    err = lib().hipStreamQuery(ctypes.c_void_p(s))
+    if err == 0:
+        return True
+    if err == 600:  # hipErrorNotReady
+        return False
+    _check(err, "hipStreamQuery")
+    return False
+
+
 def stream_synchronize(s: int) -> None:
     _check(lib().hipStreamSynchronize(ctypes.c_void_p(s)), "hipStreamSynchronize")
 

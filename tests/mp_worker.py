@@ -89,6 +89,47 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             if int(ish.get_param("flags_kind")) != want:
                 fails.append(f"pe{pe} flags_kind {ish.get_param('flags_kind')} != agreed {want}")
 
+        if "sbrelease" in scenarios:
+            # The stream barrier's escape hatch (set_param "stream_barrier_release"): PE 0 enters a
+            # stream-memory-op barrier the others never join; its stream must stay blocked (no
+            # timeout in that barrier), then move on once released; resync agrees the barrier
+            # epochs again and a barrier of every PE completes.
+            import time as _t
+            sst = hip.stream_create()
+            ish.ishmem_barrier_all()
+            ish.set_param("barrier_kind", 1)
+            if pe == 0:
+                if ish.team_sync_on_stream(0, None, sst) != 0:
+                    fails.append(f"pe0 sbrelease: enqueue failed: {ish.last_error()}")
+                _t.sleep(1.0)
+                if hip.stream_query(sst):
+                    fails.append("pe0 sbrelease: a barrier nobody joined completed")
+                if ish.set_param("stream_barrier_release", 0) != 0:
+                    fails.append(f"pe0 sbrelease: release failed: {ish.last_error()}")
+                t0 = _t.monotonic()
+                while not hip.stream_query(sst) and _t.monotonic() - t0 < 10:
+                    _t.sleep(0.01)
+                if not hip.stream_query(sst):
+                    fails.append("pe0 sbrelease: stream still blocked after the release")
+            # PE 0 is one stream barrier ahead: the kernel barrier (its own epochs) lines the PEs up,
+            # then resync agrees the stream-barrier epochs (the maximum).
+            ish.set_param("barrier_kind", 0)
+            ish.ishmem_barrier_all()
+            if ish.resync() != 0:
+                fails.append(f"pe{pe} sbrelease: resync failed: {ish.last_error()}")
+            ish.set_param("barrier_kind", 1)
+            if ish.team_sync_on_stream(0, None, sst) != 0:
+                fails.append(f"pe{pe} sbrelease: barrier after resync failed: {ish.last_error()}")
+            t0 = _t.monotonic()
+            while not hip.stream_query(sst) and _t.monotonic() - t0 < 20:
+                _t.sleep(0.01)
+            if not hip.stream_query(sst):
+                fails.append(f"pe{pe} sbrelease: the all-PE stream barrier after resync did not complete")
+                ish.set_param("stream_barrier_release", 0)
+            hip.stream_synchronize(sst)
+            hip.stream_destroy(sst)
+            ish.set_param("barrier_kind", 0)
+
         if "phaseevents" in scenarios:
             # The measurement hook: a phased reduce with events between its five launches.
             import ctypes

@@ -190,6 +190,13 @@ def test_phased_path_with_stream_memop_barriers(npes):
                              "ISHMEM_ONESHOT_P2_MAX_BYTES": 0, "ISHMEM_MAX_BLOCKS": 64}, timeout=400)
 
 
+@pytest.mark.parametrize("npes", [2, 3])
+def test_stream_barrier_release_unblocks_a_barrier_nobody_joined(npes):
+    # The stream barrier has no timeout; bench.py's probe relies on this escape hatch to keep a
+    # barrier that never completes from hanging the measured line.
+    run_pes(npes, ["sbrelease", "golden"], env={"ISHMEM_PHASED_MIN_BYTES": 0}, timeout=180)
+
+
 @pytest.mark.parametrize("npes", [2, 4])
 def test_phased_path_with_nontemporal_peer_loads(npes):
     # The measurement-only mode the N > 1 bench times over xGMI (ISHMEM_PHASED_PEER_NT /
