@@ -87,10 +87,23 @@ std::string ipc_hint()
     return h;
 }
 
+// ISHMEM_DEBUG: the reference's boolean (src/ishmem/env_defs.h:10, parsed by
+// src/env_utils.cpp:138-149: "0" / "false" off, any other value on); a decimal value above 1 is
+// this library's more verbose level.
+int debug_level()
+{
+    const char *s = getenv("ISHMEM_DEBUG");
+    if (!s || !*s) return 0;
+    char *end = nullptr;
+    const long v = strtol(s, &end, 10);
+    if (end != s && *end == '\0') return v > 0 ? (int) std::min<long>(v, 1 << 20) : 0;
+    return strcasecmp(s, "false") == 0 ? 0 : 1;
+}
+
 int fail(const std::string &msg)
 {
     g_last_error = msg;
-    if (getenv("ISHMEM_DEBUG") && atoi(getenv("ISHMEM_DEBUG")) > 0)
+    if (debug_level() > 0)
         fprintf(stderr, "[ishmem_amd] %s\n", msg.c_str());
     return 1;
 }
@@ -824,12 +837,12 @@ struct CallPins {
         const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterDefault);
         if (e != hipSuccess) {
             (void) hipGetLastError();
-            if (getenv("ISHMEM_DEBUG") && atoi(getenv("ISHMEM_DEBUG")) > 0)
+            if (debug_level() > 0)
                 fprintf(stderr, "[ishmem_amd] hipHostRegister(%p, %zu): %s (synchronous copies)\n", p, bytes,
                         hipGetErrorString(e));
             return;
         }
-        if (getenv("ISHMEM_DEBUG") && atoi(getenv("ISHMEM_DEBUG")) > 1)
+        if (debug_level() > 1)
             fprintf(stderr, "[ishmem_amd] page-locked %p, %zu bytes for the call\n", p, bytes);
         (pinned[0] ? pinned[1] : pinned[0]) = p;
     }
@@ -1472,7 +1485,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.timeout_ms = std::max<long long>(1, env_ll("ISHMEM_TIMEOUT_MS", 60000));
     s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes,
                                          std::max<long long>(0, env_bytes("ISHMEM_LL_MAX_BYTES", (long long) kLLDefaultBytes)));
-    s.debug = (int) env_ll("ISHMEM_DEBUG", 0);
+    s.debug = debug_level();
     s.trace = nullptr;
     s.stream_order = env_ll("ISHMEM_STREAM_ORDER", 0) != 0;
     s.oneshot_p2 = std::max<long long>(0, env_bytes("ISHMEM_ONESHOT_P2_MAX_BYTES", 64ll << 20));

@@ -29,7 +29,7 @@ LAUNCH_VARS = ("ISHMEM_PE", "ISHMEM_NPES", "ISHMEM_DEVICE", "ISHMEM_BOOTSTRAP_KE
                "SLURM_NPROCS", "SLURM_LOCALID", "SLURM_JOB_ID", "SLURM_STEP_ID", "SLURM_NTASKS_PER_NODE",
                "SLURM_STEP_NUM_TASKS", "SLURM_STEP_NUM_NODES", "ISHMEM_ENABLE_GPU_IPC",
                "ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "ISHMEM_WAIT_SLOTS", "ISHMEM_TEST_PCI_BUS",
-               "ISHMEM_TEST_FLAGS_UNAVAILABLE", "GPU_MAX_HW_QUEUES", "ISHMEM_BARRIER_KIND")
+               "ISHMEM_TEST_FLAGS_UNAVAILABLE", "GPU_MAX_HW_QUEUES", "ISHMEM_BARRIER_KIND", "ISHMEM_DEBUG")
 
 # One process: what ishmemi_c_init would use, then (optionally) the native bootstrap's allgather
 # among the PEs it names.
@@ -193,6 +193,8 @@ print("rc=%d|%s" % (rc, L.ishmemi_c_last_error().decode()))
     ("ISHMEM_ENABLE_GPU_IPC", "0", True), ("ISHMEM_ENABLE_GPU_IPC", "false", True),
     ("ISHMEM_ENABLE_GPU_IPC", "1", False), ("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "1", True),
     ("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "FALSE", False), ("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "0", False),
+    # ISHMEM_DEBUG is the reference's boolean (env_utils.cpp:138-149): "true" / "yes" are valid
+    ("ISHMEM_DEBUG", "true", False), ("ISHMEM_DEBUG", "yes", False), ("ISHMEM_DEBUG", "2", False),
     # the team-barrier kind: kernel (default) or stream memory operations
     ("ISHMEM_BARRIER_KIND", "stream", False), ("ISHMEM_BARRIER_KIND", "Kernel", False),
     ("ISHMEM_BARRIER_KIND", "cp", True),
