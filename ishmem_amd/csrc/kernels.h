@@ -240,6 +240,11 @@ int device_share();
 constexpr int kWaitSlotsDefault = 16;
 void set_wait_slots(int slots);
 int wait_slots();
+// Tests only (set_param "realign_grid_cap"): at most this many workgroups for the realigned
+// kernels (0 = no cap), so their grid-stride loops — which otherwise run only past 2^31 items —
+// are exercised at test sizes.
+void set_realign_grid_cap(int cap);
+int realign_grid_cap();
 // Test hook: `grid` workgroups that each hold half a CU (1024 work-items, 80 KiB LDS) for `usec`.
 hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s);
 hipError_t launch_produce_u32(uint32_t *dst, const uint32_t *a, const uint32_t *b, uint64_t n, hipStream_t s);

@@ -12,6 +12,9 @@ void set_device_share(int share) { g_device_share = share < 1 ? 1 : share; }
 int device_share() { return g_device_share; }
 void set_wait_slots(int slots) { g_wait_slots = slots < 1 ? 1 : slots; }
 int wait_slots() { return g_wait_slots; }
+int g_realign_grid_cap = 0;
+void set_realign_grid_cap(int cap) { g_realign_grid_cap = cap < 0 ? 0 : cap; }
+int realign_grid_cap() { return g_realign_grid_cap; }
 
 #define ISHMEMI_DECL_OP(N)                                                                         \
     hipError_t launch_allreduce_op##N(int dt, bool vec, const ReduceArgs &a, int grid,             \

@@ -1337,8 +1337,9 @@ hipError_t rs_phase_t(const PhaseArgs &a, hipStream_t s)
         hipLaunchKernelGGL(kernel, dim3(phase_grid(kernel, len)), dim3(kFaninBlock), 0, s, a);
     };
     if (a.shift) {
-        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((len + kRsRealignBlock - 1) / kRsRealignBlock,
-                                                                    (1ull << 31) / kRsRealignBlock));
+        uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((len + kRsRealignBlock - 1) / kRsRealignBlock,
+                                                              (1ull << 31) / kRsRealignBlock));
+        if (realign_grid_cap() > 0) g = std::min<uint64_t>(g, (uint64_t) realign_grid_cap());
         hipLaunchKernelGGL((rs_phase_realign_kernel<T, OP>), dim3((unsigned) g), dim3(kRsRealignBlock), 0, s, a);
     } else if (a.p == 2) go(rs_phase_kernel<T, OP, 2>);
     else if (a.p == 4) go(rs_phase_kernel<T, OP, 4>);
@@ -1554,6 +1555,7 @@ template <typename T, int OP>
 hipError_t fi_t(bool vec, const FaninArgs &a, int grid, hipStream_t s)
 {
     if (a.realign) {
+        if (realign_grid_cap() > 0) grid = std::min(grid, realign_grid_cap());
         if (a.nsrc == 1) hipLaunchKernelGGL((fanin_realign_kernel<T, OP, 1>), dim3(grid), dim3(kRealignBlock), 0, s, a);
         else if (a.nsrc == 2) hipLaunchKernelGGL((fanin_realign_kernel<T, OP, 2>), dim3(grid), dim3(kRealignBlock), 0, s, a);
         else return hipErrorInvalidValue;

@@ -89,6 +89,11 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             if int(ish.get_param("flags_kind")) != want:
                 fails.append(f"pe{pe} flags_kind {ish.get_param('flags_kind')} != agreed {want}")
 
+        if "realigncap" in scenarios:
+            # Tests only: at most 3 workgroups for the realigned kernels, so the realigned
+            # reduce-scatter's grid-stride loop (edge[] reuse between passes) runs at test sizes.
+            ish.set_param("realign_grid_cap", 3)
+
         if "sbrelease" in scenarios:
             # The stream barrier's escape hatch (set_param "stream_barrier_release"): PE 0 enters a
             # stream-memory-op barrier the others never join; its stream must stay blocked (no

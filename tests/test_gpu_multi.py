@@ -190,6 +190,16 @@ def test_phased_path_with_stream_memop_barriers(npes):
                              "ISHMEM_ONESHOT_P2_MAX_BYTES": 0, "ISHMEM_MAX_BLOCKS": 64}, timeout=400)
 
 
+@pytest.mark.parametrize("npes", [2, 3, 8])
+def test_realigned_reduce_scatter_grid_stride_loop(npes):
+    # The phased path forced, sources on other 16-B phases than dest (offsets_large), with the
+    # realigned reduce-scatter capped at 3 workgroups: its grid-stride loop, which otherwise runs
+    # only past 2^31 items per chunk, makes several passes per workgroup.
+    run_pes(npes, ["realigncap", "offsets_large"],
+            env={"ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_ONESHOT_P2_MAX_BYTES": 0},
+            timeout=300)
+
+
 @pytest.mark.parametrize("npes", [2, 3])
 def test_stream_barrier_release_unblocks_a_barrier_nobody_joined(npes):
     # The stream barrier has no timeout; bench.py's probe relies on this escape hatch to keep a

@@ -260,3 +260,38 @@ def test_device_pattern_checker_counts_wrong_bytes(ish, npd):
             assert dev == host and 3 <= dev <= 4, (dev, host)
     finally:
         ish.ishmem_free(d)
+
+
+@pytest.mark.parametrize("dt", [0, 2, 9])
+def test_realigned_kernels_grid_stride_loop(ish, dt):
+    """The realigned fan-in's grid-stride loop (with the LDS edge slots reused between passes)
+    otherwise runs only past 2^31 items; set_param("realign_grid_cap") caps its grid at 1 / 3 / 7
+    workgroups so every workgroup makes several passes.  Copy and a + b, sources on other 16-B
+    phases than dest, bit-exact against the oracle, bytes around dest untouched."""
+    from ishmem_amd import hip
+    es = np.dtype(oracle.NP[dt]).itemsize
+    n = (8192 * 9 + 4099) // es + 3
+    pad = 64
+    base = [hip.malloc(n * es + 2 * pad) for _ in range(3)]
+    try:
+        for cap in (1, 3, 7):
+            assert ish.set_param("realign_grid_cap", cap) == 0
+            for o in ((es, 0, 2 * es % 16), (0, 3 * es % 16, es)):
+                srcs = [oracle.fill_random(dt, 100 * cap + 7 * i + o[i], n) for i in range(2)]
+                for i in range(2):
+                    hip.upload(base[i] + pad + o[i], srcs[i])
+                for k in (1, 2):
+                    hip.memset(base[2], 0xA5, n * es + 2 * pad)
+                    assert ish.combine("sum" if dt != 0 else "or", DNAMES[dt], base[2] + pad + o[2],
+                                       [base[i] + pad + o[i] for i in range(k)], n) == 0, ish.last_error()
+                    hip.synchronize()
+                    got = hip.download(base[2] + pad + o[2], n, oracle.NP[dt])
+                    op = oracle.OPS["sum"] if dt != 0 else oracle.OPS["or"]
+                    assert _bits_equal(got, oracle.reduce_fold(op, dt, srcs[:k], 0)), (dt, cap, o, k)
+                    raw = hip.download(base[2], n * es + 2 * pad, np.uint8)
+                    lo, hi = pad + o[2], pad + o[2] + n * es
+                    assert (raw[:lo] == 0xA5).all() and (raw[hi:] == 0xA5).all(), (dt, cap, o, k)
+    finally:
+        ish.set_param("realign_grid_cap", 0)
+        for b in base:
+            hip.free(b)

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                                      \
@@ -115,8 +116,60 @@ int main(int argc, char **argv)
             CK(hipStreamSynchronize(B));
             kk_us = (now_us() - t0) / rounds;
         }
-        printf("%-13s self %.2f us/pair  pingpong %.2f us/barrier  kernel pingpong %.2f us/barrier\n", k.name,
-               self_us, pp_us, kk_us);
+        // hipStreamBatchMemOp: the write and the wait of one side as ONE call (one submission).
+        double bb_us = -1, bs_us = -1;
+        if (wb) {
+            CK(hipMemset(w, 0, bytes));
+            CK(hipDeviceSynchronize());
+            hipError_t eb = hipSuccess;
+            t0 = now_us();
+            for (uint32_t r = 1; r <= (uint32_t) rounds && eb == hipSuccess; ++r) {
+                hipStreamBatchMemOpParams pa[2], pb[2];
+                memset(pa, 0, sizeof(pa));
+                memset(pb, 0, sizeof(pb));
+                pa[0].writeValue.operation = hipStreamMemOpWriteValue32;
+                pa[0].writeValue.address = (hipDeviceptr_t) wa;
+                pa[0].writeValue.value = r;
+                pa[1].waitValue.operation = hipStreamMemOpWaitValue32;
+                pa[1].waitValue.address = (hipDeviceptr_t) wb;
+                pa[1].waitValue.value = r;
+                pa[1].waitValue.flags = hipStreamWaitValueGte;
+                pb[0] = pa[0];
+                pb[0].writeValue.address = (hipDeviceptr_t) wb;
+                pb[1] = pa[1];
+                pb[1].waitValue.address = (hipDeviceptr_t) wa;
+                eb = hipStreamBatchMemOp(A, 2, pa, 0);
+                if (eb == hipSuccess) eb = hipStreamBatchMemOp(B, 2, pb, 0);
+            }
+            if (eb != hipSuccess) {
+                printf("%-13s hipStreamBatchMemOp: %s\n", k.name, hipGetErrorString(eb));
+                (void) hipGetLastError();
+            } else {
+                CK(hipStreamSynchronize(A));
+                CK(hipStreamSynchronize(B));
+                bb_us = (now_us() - t0) / rounds;
+            }
+            // self: one batch of a write and a satisfied wait on one stream
+            t0 = now_us();
+            for (uint32_t r = 1; r <= (uint32_t) rounds && eb == hipSuccess; ++r) {
+                hipStreamBatchMemOpParams pa[2];
+                memset(pa, 0, sizeof(pa));
+                pa[0].writeValue.operation = hipStreamMemOpWriteValue32;
+                pa[0].writeValue.address = (hipDeviceptr_t) wa;
+                pa[0].writeValue.value = (uint32_t) rounds + r;
+                pa[1].waitValue.operation = hipStreamMemOpWaitValue32;
+                pa[1].waitValue.address = (hipDeviceptr_t) wa;
+                pa[1].waitValue.value = (uint32_t) rounds + r;
+                pa[1].waitValue.flags = hipStreamWaitValueGte;
+                eb = hipStreamBatchMemOp(A, 2, pa, 0);
+            }
+            if (eb == hipSuccess) {
+                CK(hipStreamSynchronize(A));
+                bs_us = (now_us() - t0) / rounds;
+            }
+        }
+        printf("%-13s self %.2f us/pair  pingpong %.2f us/barrier  kernel pingpong %.2f us/barrier  "
+               "batch pingpong %.2f us/barrier  batch self %.2f us\n", k.name, self_us, pp_us, kk_us, bb_us, bs_us);
         CK(hipFree(w));
     }
     return 0;
