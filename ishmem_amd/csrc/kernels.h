@@ -245,6 +245,11 @@ int wait_slots();
 // are exercised at test sizes.
 void set_realign_grid_cap(int cap);
 int realign_grid_cap();
+// The phased fcollect / collect moves members whose addresses or counts are not 16-B aligned with
+// realigned 16-B loads (kernels_coll.hip collect_phase_realign_kernel); 0 (set_param
+// "collect_realign", A/B only) keeps the narrow 4- / 1-byte items.
+void set_collect_realign(int on);
+int collect_realign();
 // Test hook: `grid` workgroups that each hold half a CU (1024 work-items, 80 KiB LDS) for `usec`.
 hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s);
 hipError_t launch_produce_u32(uint32_t *dst, const uint32_t *a, const uint32_t *b, uint64_t n, hipStream_t s);

@@ -15,6 +15,9 @@ int wait_slots() { return g_wait_slots; }
 int g_realign_grid_cap = 0;
 void set_realign_grid_cap(int cap) { g_realign_grid_cap = cap < 0 ? 0 : cap; }
 int realign_grid_cap() { return g_realign_grid_cap; }
+int g_collect_realign = 1;
+void set_collect_realign(int on) { g_collect_realign = on != 0; }
+int collect_realign() { return g_collect_realign; }
 
 #define ISHMEMI_DECL_OP(N)                                                                         \
     hipError_t launch_allreduce_op##N(int dt, bool vec, const ReduceArgs &a, int grid,             \

@@ -102,6 +102,51 @@ __global__ __launch_bounds__(kFaninBlock) void collect_phase_kernel(CollectArgs 
     }
 }
 
+// The phased fcollect / collect when some source, dest offset or count is not 16-B aligned
+// (round 5): instead of narrowing every member's copy to 4- or 1-byte items (2 PEs x 64 MiB on one
+// GPU: 86 us aligned, 179 us with 4-byte items, 345 us with 1-byte items, tools/collect_probe.py),
+// member j's dest is peeled to the 16-B grid byte-wise (head, and the tail after the last whole
+// vector) and its body is moved in 16-B items with the realigned loads of the fan-in
+// (kernels_impl.h realign_issue / realign_finish: aligned source vectors, the in-wave neighbour by
+// DPP, the vector past the wave's end loaded by lane 63, a funnel shift by the member's own byte
+// shift).  Same block map as collect_phase_kernel: workgroup w, member (me + 1 + w mod p) mod p,
+// its 1 KiB block w / p; the member's block 0 also moves the head / tail bytes.
+__global__ __launch_bounds__(kFaninBlock) void collect_phase_realign_kernel(CollectArgs a, uint64_t blocks)
+{
+    __shared__ u32x4 edge[2];
+    const int p = a.p;
+    const uint32_t lane = threadIdx.x;
+    for (uint64_t w = blockIdx.x; w < (uint64_t) p * blocks; w += gridDim.x) {
+        const int j = (a.me + 1 + (int) (w % (uint64_t) p)) % p;
+        const uint64_t nb = a.nbytes[j];
+        char *dj = a.dst + a.dst_off[j];
+        const uint64_t h = std::min<uint64_t>(nb, (16 - (uint64_t) (uintptr_t) dj % 16) % 16);
+        const uint64_t nitems = (nb - h) / 16;
+        const uint64_t tail = nb - h - nitems * 16;
+        const uint64_t blk = w / (uint64_t) p;
+        const uint64_t i0 = blk * kFaninBlock;
+        const bool local = j == a.me;
+        if (i0 < nitems) {  // workgroup-uniform
+            const uint64_t wo = h + i0 * 16;
+            const uint32_t shift = (uint32_t) (((uint64_t) (uintptr_t) a.src[j] + wo) % 16);
+            u32x4 A, B;
+            if (local) realign_issue<kNonTemporal, kFaninBlock>(a.src[j], shift, nb, wo, edge, A, B);
+            else realign_issue<kSysCoherent, kFaninBlock>(a.src[j], shift, nb, wo, edge, A, B);
+            __syncthreads();
+            const u32x4 x = realign_finish(edge, A, B, shift);
+            if (i0 + lane < nitems) wt_store(make_rsrc(uniform_ptr(dj + wo)), lane * 16u, x);
+            __syncthreads();  // edge[] is rewritten by this workgroup's next block
+        }
+        if (blk == 0 && (h || tail)) {
+            const uint64_t tb = h + nitems * 16;
+            if (lane < h) dj[lane] = (char) (local ? a.src[j][lane] : cload<uint8_t>(make_rsrc(uniform_ptr(a.src[j])), lane));
+            if (lane < tail)
+                dj[tb + lane] = (char) (local ? a.src[j][tb + lane]
+                                              : cload<uint8_t>(make_rsrc(uniform_ptr(a.src[j] + tb)), lane));
+        }
+    }
+}
+
 // Member j's `nbytes` at `src` -> dst (local), U-byte items, tiles b, b + G, ... of workgroup b.
 template <int U>
 __device__ __forceinline__ void collect_member(const char *src, char *dst, uint64_t nbytes, bool local,
@@ -499,6 +544,7 @@ hipError_t launch_collect_phase(const CollectArgs &a, hipStream_t s)
     const uint64_t blocks = (maxb + 1023) / 1024;  // 1 KiB blocks of the largest member
     const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t) a.p * blocks, (uint64_t) kFaninMaxGrid));
     if (a.unit == 16) hipLaunchKernelGGL(collect_phase_kernel<16>, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
+    else if (collect_realign()) hipLaunchKernelGGL(collect_phase_realign_kernel, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
     else if (a.unit == 4) hipLaunchKernelGGL(collect_phase_kernel<4>, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
     else hipLaunchKernelGGL(collect_phase_kernel<1>, dim3((unsigned) g), dim3(kFaninBlock), 0, s, a, blocks);
     return hipGetLastError();

@@ -2694,6 +2694,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "phased_peer_nt") s.phased_peer_nt = value != 0;
     else if (n == "barrier_kind") s.barrier_kind = value != 0 ? 1 : 0;  // measurement: set alike on every PE
     else if (n == "realign_grid_cap") set_realign_grid_cap((int) std::min<long long>(std::max<long long>(value, 0), 1 << 30));
+    else if (n == "collect_realign") set_collect_realign((int) (value != 0));
     else if (n == "stream_barrier_release") {
         // Escape hatch of the stream barrier, which has no timeout (team_barrier): store the team's
         // latest stream-barrier epoch into every slot of this PE's own wait row, so a stream stuck
@@ -2736,6 +2737,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "phased_peer_nt") return s.phased_peer_nt;
     if (n == "barrier_kind") return s.barrier_kind;
     if (n == "realign_grid_cap") return realign_grid_cap();
+    if (n == "collect_realign") return collect_realign();
     if (n == "flags_fine_grained") return s.flags_kind != kFlagsCoarse ? 1 : 0;
     if (n == "flags_kind") return s.flags_kind;
     if (n == "staging_bytes") return (long long) s.staging_bytes;
