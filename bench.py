@@ -224,7 +224,7 @@ def legs_healthy(ish, dist) -> bool:
     return max_over_ranks(dist, [device_errors(ish)])[0] == 0
 
 
-def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max):
+def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max, share: int = 1):
     """BASELINE configs[4]: min/max/prod x int32/float64, 4 KiB .. nbytes_max per PE in steps of 4x:
     us per call (max over ranks), algbw, and a check of EVERY word of dest on every rank at every
     size (the device checker, tests/cpp/pattern_check.hip) against the team-order fold of the
@@ -272,8 +272,12 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max):
                     wins += [(int(x), 4096) for x in np.random.default_rng(5).integers(0, n - 4096, 8)]
                 bad = sum(sc.count_wrong(hip, dst, op, npd, world, lo, m) for lo, m in wins)
                 bad = int(max_over_ranks(dist, [float(bad)])[0])
+                _, t_roof = roofline(world, share, nb, us * 1e-3)
                 out.append({"op": op, "dtype": dtn, "bytes": nb, "us": round(us, 2),
                             "algbw_GiBps": round(nb / GiB / (us * 1e-6), 2),
+                            # t_roof / t: the same bound as the line's roofline (xGMI links one PE
+                            # per GPU, device HBM when PEs share a GPU); mid sizes are latency-bound
+                            "roofline_frac": round(t_roof / (us * 1e-6), 3),
                             "checked": bad == 0, "words_checked": sum(m for _, m in wins),
                             "checker": sc.checker_kind(npd)})
                 nb *= 4
@@ -948,7 +952,7 @@ def main() -> int:
         log("config-5 sweep")
         # BASELINE configs[4] (min/max/prod x int32/float64 across the PEs), 4 KiB .. 4 GiB per PE.
         try:
-            extra["config5_sweep"] = config5_sweep(ish, hip, world, rank, dist, stream, sweep_max)
+            extra["config5_sweep"] = config5_sweep(ish, hip, world, rank, dist, stream, sweep_max, share)
         except Exception as ex:
             extra["config5_sweep"] = {"error": str(ex)}
 
