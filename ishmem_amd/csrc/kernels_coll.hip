@@ -15,14 +15,28 @@ namespace {
 // All-gather of the sources: workgroup b copies tiles t == b (mod G) of every member's source,
 // member order rotated by workgroup (all links busy), local slot included.  Only remote LOADS;
 // between launch_start and launch_finish nothing waits, so the static tile split is safe.
+__device__ void collect_member_realign(const char *src, char *dst, uint64_t nb, bool local, uint32_t b, uint64_t G,
+                                       u32x4 *edge);
+
+// U = 0: members off the 16-B grid moved with realigned 16-B loads (collect_member_realign).
 template <int U>
 __global__ __launch_bounds__(kBlock) void collect_kernel(CollectArgs a)
 {
-    using Item = std::conditional_t<U == 16, Vec<uint32_t>, std::conditional_t<U == 4, uint32_t, uint8_t>>;
+    using Item = std::conditional_t<U == 16 || U == 0, Vec<uint32_t>, std::conditional_t<U == 4, uint32_t, uint8_t>>;
     const int tid = threadIdx.x, b = blockIdx.x;
     const uint64_t G = gridDim.x;
     const uint32_t ep = kernel_epoch(a);
     const bool ok = launch_start(a, ep);
+    if constexpr (U == 0) {
+        __shared__ u32x4 edge[kBlock / 64 + 1];
+        if (ok)
+            for (int k = 0; k < a.p; ++k) {
+                const int j = (a.me + (b + k)) % a.p;
+                collect_member_realign(a.src[j], a.dst + a.dst_off[j], a.nbytes[j], j == a.me, (uint32_t) b, G, edge);
+            }
+        launch_finish(a, ep);
+        return;
+    }
     if (ok) {
         for (int k = 0; k < a.p; ++k) {
             const int j = (a.me + (b + k)) % a.p;
@@ -181,6 +195,36 @@ __device__ __forceinline__ void collect_member(const char *src, char *dst, uint6
     }
 }
 
+// Member j's `nb` bytes at `src` -> dst with dst off the 16-B grid relative to src (round 5):
+// dst is peeled to the 16-B grid (head bytes, and the tail after the last whole vector, copied by
+// workgroup 0), the body moves in 4 KiB blocks b, b + G, ... of 16-B items with the realigned
+// loads (kernels_impl.h realign_issue / realign_finish, kBlock threads).  Every thread calls it.
+__device__ void collect_member_realign(const char *src, char *dst, uint64_t nb, bool local, uint32_t b, uint64_t G,
+                                       u32x4 *edge)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t h = min(nb, (16 - (uint64_t) (uintptr_t) dst % 16) % 16);
+    const uint64_t nitems = (nb - h) / 16;
+    const uint64_t tail = nb - h - nitems * 16;
+    for (uint64_t blk = b; blk * kBlock < nitems; blk += G) {
+        const uint64_t i0 = blk * kBlock, wo = h + i0 * 16;
+        const uint32_t shift = (uint32_t) (((uint64_t) (uintptr_t) src + wo) % 16);
+        u32x4 A, B;
+        if (local) realign_issue<kNonTemporal, kBlock>(src, shift, nb, wo, edge, A, B);
+        else realign_issue<kSysCoherent, kBlock>(src, shift, nb, wo, edge, A, B);
+        __syncthreads();
+        const u32x4 x = realign_finish(edge, A, B, shift);
+        if (i0 + tid < nitems) *(u32x4 *) (dst + wo + tid * 16u) = x;
+        __syncthreads();  // edge[] is rewritten by the next block
+    }
+    if (b == 0) {
+        const uint64_t tb = h + nitems * 16;
+        if (tid < h) dst[tid] = (char) (local ? src[tid] : cload<uint8_t>(make_rsrc(uniform_ptr(src)), tid));
+        if (tid < tail)
+            dst[tb + tid] = (char) (local ? src[tb + tid] : cload<uint8_t>(make_rsrc(uniform_ptr(src + tb)), tid));
+    }
+}
+
 // Stream-ordered collect (ishmemx_<TN>_collect_on_queue, src/ishmemx.h): the counts are not
 // known when the launch is enqueued.  Every workgroup first stores this member's count into its
 // symmetric slot (system-scope, drained) — any workgroup may be the one that announces the
@@ -192,6 +236,7 @@ __device__ __forceinline__ void collect_member(const char *src, char *dst, uint6
 __global__ __launch_bounds__(kBlock) void collect_dyn_kernel(CollectArgs a)
 {
     __shared__ uint64_t s_cnt[kMaxPes];
+    __shared__ u32x4 edge[kBlock / 64 + 1];  // a.unit == 0: realigned members (collect_member_realign)
     const uint32_t b = blockIdx.x;
     const uint64_t G = gridDim.x;
     const uint32_t ep = kernel_epoch(a);
@@ -210,6 +255,7 @@ __global__ __launch_bounds__(kBlock) void collect_dyn_kernel(CollectArgs a)
             const uint64_t n = s_cnt[j];
             const uint64_t al = (uint64_t) a.src[j] | ((uint64_t) a.dst + off) | n;
             if ((al & 15) == 0) collect_member<16>(a.src[j], a.dst + off, n, j == a.me, b, G);
+            else if (a.unit == 0) collect_member_realign(a.src[j], a.dst + off, n, j == a.me, b, G, edge);
             else if ((al & 3) == 0) collect_member<4>(a.src[j], a.dst + off, n, j == a.me, b, G);
             else collect_member<1>(a.src[j], a.dst + off, n, j == a.me, b, G);
         }
@@ -533,6 +579,7 @@ hipError_t launch_res(K kernel, const A &a, int grid, hipStream_t s)
 hipError_t launch_collect(const CollectArgs &a, int grid, hipStream_t s)
 {
     if (a.unit == 16) return launch_res(collect_kernel<16>, a, grid, s);
+    if (collect_realign()) return launch_res(collect_kernel<0>, a, grid, s);
     if (a.unit == 4) return launch_res(collect_kernel<4>, a, grid, s);
     return launch_res(collect_kernel<1>, a, grid, s);
 }
@@ -552,7 +599,9 @@ hipError_t launch_collect_phase(const CollectArgs &a, hipStream_t s)
 
 hipError_t launch_collect_dyn(const CollectArgs &a, int grid, hipStream_t s)
 {
-    return launch_res(collect_dyn_kernel, a, grid, s);
+    CollectArgs b = a;
+    b.unit = collect_realign() ? 0 : 1;  // members off the 16-B grid: realigned (0) or narrow items
+    return launch_res(collect_dyn_kernel, b, grid, s);
 }
 
 hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s)
