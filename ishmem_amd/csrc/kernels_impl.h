@@ -1372,13 +1372,36 @@ __device__ __forceinline__ uint64_t fold8(uint64_t acc, uint64_t x)
 
 // The grid is capped by the waiting footprint (resident_blocks_of), so a thread may own several
 // items (t, t + G*kBlock, ...): it pushes all of them before polling for any.
+// Item `off` (8 payload bytes, or the `valid` < 8 of the ragged last item) of the source.  Items
+// sit at multiples of 8 bytes from element 0, so elements never straddle them whatever the
+// array's address; the address only picks the load width (round 5: 4-B aligned arrays — a float
+// array 4 B off an 8-B boundary — took the persistent kernel before, 8.5 vs 4.5 us at 64 KiB).
 __device__ __forceinline__ uint64_t ll_load(const LLArgs &a, uint64_t off, uint64_t valid)
 {
-    if (valid == 8) return *(const uint64_t *) (a.src + off);
-    // Ragged last item: byte assembly (a variable-length memcpy would go through scratch).
+    const char *p = a.src + off;
+    if (valid == 8) {
+        if (((uintptr_t) p & 7) == 0) return *(const uint64_t *) p;
+        if (((uintptr_t) p & 3) == 0)
+            return (uint64_t) ((const uint32_t *) p)[0] | ((uint64_t) ((const uint32_t *) p)[1] << 32);
+    }
+    // Ragged last item or a byte-aligned array: byte assembly (a variable-length memcpy would go
+    // through scratch).
     uint64_t mine = 0;
-    for (uint32_t k = 0; k < (uint32_t) valid; ++k) mine |= (uint64_t) (uint8_t) a.src[off + k] << (8 * k);
+    for (uint32_t k = 0; k < (uint32_t) valid; ++k) mine |= (uint64_t) (uint8_t) p[k] << (8 * k);
     return mine;
+}
+
+__device__ __forceinline__ void ll_store(const LLArgs &a, uint64_t off, uint64_t valid, uint64_t v)
+{
+    char *p = a.dst + off;
+    if (valid == 8 && ((uintptr_t) p & 7) == 0) {
+        *(uint64_t *) p = v;
+    } else if (valid == 8 && ((uintptr_t) p & 3) == 0) {
+        ((uint32_t *) p)[0] = (uint32_t) v;
+        ((uint32_t *) p)[1] = (uint32_t) (v >> 32);
+    } else {
+        for (uint32_t k = 0; k < (uint32_t) valid; ++k) p[k] = (char) (v >> (8 * k));
+    }
 }
 
 template <typename T, int OP>
@@ -1429,13 +1452,7 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
             }
             acc = (j == 0) ? x : fold8<T, OP>(acc, x);
         }
-        if (ok) {
-            if (valid == 8) {
-                *(uint64_t *) (a.dst + off) = acc;
-            } else {
-                for (uint32_t k = 0; k < (uint32_t) valid; ++k) a.dst[off + k] = (char) (acc >> (8 * k));
-            }
-        }
+        if (ok) ll_store(a, off, valid, acc);
     }
     // *ret was zeroed by the caller: any thread that failed marks it (sticky over launches).
     if (!ok && a.ret) __hip_atomic_fetch_or(a.ret, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

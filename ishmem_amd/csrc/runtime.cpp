@@ -595,12 +595,15 @@ int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)
     return 0;
 }
 
-// Small payloads (<= ll_max_bytes, 8-B aligned, device memory anywhere): one-hop push of
-// {data, epoch} granules into the peers' rings, no barriers (ll_kernel).
+// Small payloads (<= ll_max_bytes, device memory anywhere, any element-aligned address — the
+// kernel picks 8-, 4- or 1-byte accesses, ll_load / ll_store): one-hop push of {data, epoch}
+// granules into the peers' rings, no barriers (ll_kernel).  The choice depends on the byte count
+// only, which every member shares.
 bool ll_eligible(const State &s, const Team &t, const void *dst, const void *src, size_t bytes)
 {
-    return t.size > 1 && bytes > 0 && (long long) bytes <= s.ll_max_bytes &&
-           bytes <= kLLMaxBytes && (((uintptr_t) dst | (uintptr_t) src) & 7) == 0;
+    (void) dst;
+    (void) src;
+    return t.size > 1 && bytes > 0 && (long long) bytes <= s.ll_max_bytes && bytes <= kLLMaxBytes;
 }
 
 // Collectives of one PE run in the order they were called, whatever streams they were enqueued
