@@ -310,6 +310,10 @@ struct State {
     // Measurement only (set_param "phased_peer_nt"): the phased grids load peers' bytes
     // nontemporal instead of sc0 sc1 (kernels.h PhaseArgs::peer_nt).  Must be set alike on every PE.
     int phased_peer_nt = 0;
+    // Persistent kernel with sources on another 16-B phase than dest (set_param "ar_shifted",
+    // default 1): vector items laid out by dest, the sources read with unaligned 16-B loads;
+    // 0 = the element-granular instantiation (A/B only).
+    int ar_shifted = 1;
     // Team barriers of the phased paths and ishmem_team_sync: 0 = the one-workgroup barrier
     // kernel (team_sync_kernel), 1 = stream memory operations (ISHMEM_BARRIER_KIND=stream: the
     // command processor waits, no workgroup is held; team_barrier).  Agreed at init; sb_epoch is
@@ -754,7 +758,20 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     // phased grids realign the sources (rs_phase_kernel, a.shift) instead of the persistent
     // kernel's element-granular path.
     const bool realign = !pl.vec && d0 % es == 0 && s0 % es == 0 && nb >= kRealignMinBytes;
-    if ((pl.vec || realign) && (long long) nb >= s.phased_min) {
+    if (realign && (long long) nb < s.phased_min && s.ar_shifted) {
+        // Below phased_min: the persistent kernel's vector instantiation with items laid out by
+        // dest's phase; every source is read at dest's item offsets with unaligned 16-B loads (the
+        // hardware splits a load that crosses a line: tools/realign_variants.hip "unaligned buf",
+        // 0.78 of HBM at 1 GiB against 0.84 aligned, profiles/r05/realign/).  The all-gather
+        // reads peers' dests, on dest's phase on every PE (symmetric offsets), so it stays aligned.
+        const void *dsts[1] = {dst};
+        pl = make_plan(dst, dsts, 1, n, es, t.size, s.max_blocks, 0);
+        a.head = pl.head;
+        a.nitems = pl.nitems;
+        a.tail = pl.tail;
+        a.items_per_chunk = pl.items_per_chunk;
+        a.seg_items = pl.seg_items;
+    } else if ((pl.vec || realign) && (long long) nb >= s.phased_min) {
         // From phased_min bytes: barrier, one-shot reduce-scatter, barrier, one-shot all-gather,
         // barrier (kernels_impl.h, "Phased reduce-scatter + all-gather").  The barriers carry *ret.
         // Checked before the two-member one-shot fold, which it beats from 32 MiB.
@@ -2698,6 +2715,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "barrier_kind") s.barrier_kind = value != 0 ? 1 : 0;  // measurement: set alike on every PE
     else if (n == "realign_grid_cap") set_realign_grid_cap((int) std::min<long long>(std::max<long long>(value, 0), 1 << 30));
     else if (n == "collect_realign") set_collect_realign((int) (value != 0));
+    else if (n == "ar_shifted") s.ar_shifted = value != 0;  // measurement: set alike on every PE
     else if (n == "stream_barrier_release") {
         // Escape hatch of the stream barrier, which has no timeout (team_barrier): store the team's
         // latest stream-barrier epoch into every slot of this PE's own wait row, so a stream stuck
@@ -2741,6 +2759,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "barrier_kind") return s.barrier_kind;
     if (n == "realign_grid_cap") return realign_grid_cap();
     if (n == "collect_realign") return collect_realign();
+    if (n == "ar_shifted") return s.ar_shifted;
     if (n == "flags_fine_grained") return s.flags_kind != kFlagsCoarse ? 1 : 0;
     if (n == "flags_kind") return s.flags_kind;
     if (n == "staging_bytes") return (long long) s.staging_bytes;

@@ -34,6 +34,8 @@ def main() -> None:
                     "HIP events between the phased path's five launches (rank 0's ms)")
     ap.add_argument("--emulate-share1", action="store_true",
                     help="every PE reports its own device (ISHMEM_TEST_PCI_BUS): the launch shapes of one PE per GPU")
+    ap.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
+                    help="ishmem set_param before the sweep (every PE alike), repeatable")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -54,6 +56,9 @@ def main() -> None:
     from ishmem_amd import hip
     dev = 0 if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else local
     ish.init(rank, world, dev, key)
+    for kv in args.param:
+        name, val = kv.split("=", 1)
+        ish.set_param(name, int(val))
     nmax = (args.max_mib << 20) // 4
     so, do = args.src_offset // 4, args.dst_offset // 4
     src = ish.ishmem_malloc(nmax * 4 + 64)
@@ -63,7 +68,7 @@ def main() -> None:
     if rank == 0:
         print(f"# coll={args.coll} graph={args.graph} blocking={args.blocking} pes={world} same_device={os.environ.get('ISHMEM_BENCH_SAME_DEVICE') == '1'} "
               f"ll_max_bytes={ish.get_param('ll_max_bytes')} wait_slots={ish.get_param('wait_slots')} "
-              f"device_share={ish.get_param('device_share')} src_offset={args.src_offset} dst_offset={args.dst_offset}")
+              f"device_share={ish.get_param('device_share')} src_offset={args.src_offset} dst_offset={args.dst_offset} params={args.param}")
         print("bytes,us_per_call,algbw_GiBps,ok")
     def call(n):
         if args.blocking:
