@@ -329,7 +329,8 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
                three team barriers as the one-workgroup barrier kernel (default) or as stream
                memory operations (ISHMEM_BARRIER_KIND=stream: the command processor waits);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
-      ll    - 4 / 16 / 64 KiB with the one-hop granule path on (default) and off."""
+      ll    - 4 KiB up to the granule ring's capacity (1 MiB / team size) with the one-hop granule
+              path on (default) and off."""
 
     def timed(n, iters):
         for _ in range(2):
@@ -385,9 +386,11 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     if world == 2:
         run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
         run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)
-    for nb in (4096, 16384, 65536):
-        run("ll_on", "ll_max_bytes", 65536, nb, 50)
-        run("ll_off", "ll_max_bytes", 0, nb, 50)
+    cap = int(ish.get_param("ll_capacity_bytes"))  # the ring's capacity at this team size
+    for nb in (4096, 16384, 65536, 131072, 262144, 524288):
+        if nb <= cap:
+            run("ll_on", "ll_max_bytes", cap, nb, 50)
+            run("ll_off", "ll_max_bytes", 0, nb, 50)
     return out
 
 

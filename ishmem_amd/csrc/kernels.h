@@ -82,11 +82,24 @@ struct ReduceArgs {
 };
 
 // Small-message ("LL") path: 8-byte granules {4 data bytes | 32-bit epoch} pushed into every
-// peer's fine-grained receive ring; [parity 2][sender kMaxPes][kLLGranules] u64 per team.
-constexpr size_t kLLMaxBytes = 65536;                 // LL ring capacity: payload bytes per PE
-constexpr size_t kLLDefaultBytes = 65536;             // default LL threshold (ISHMEM_LL_MAX_BYTES)
-constexpr size_t kLLGranules = kLLMaxBytes / 4;       // 4 payload bytes per granule
-constexpr size_t kLLTeamBytes = (size_t) 2 * kMaxPes * kLLGranules * 8;  // 4 MiB
+// peer's fine-grained receive ring.  One ring of kLLTeamBytes per team, laid out by the team's size
+// p as [parity 2][sender p][ll_sender_granules(p)] u64, so a sender's capacity is
+// kLLTeamBytes / (4p) payload bytes: 512 KiB at 2 PEs, 256 KiB at 4, 128 KiB at 8, 64 KiB at 16.
+// The path's link traffic is 2(p-1)·B per PE, and its crossover with the persistent kernel,
+// measured, falls as 1/p as well: the capacity is the default threshold.
+#ifndef ISHMEMI_LL_TEAM_BYTES
+#define ISHMEMI_LL_TEAM_BYTES (4u << 20)
+#endif
+constexpr size_t kLLTeamBytes = ISHMEMI_LL_TEAM_BYTES;
+__host__ __device__ constexpr uint64_t ll_sender_granules(int p)
+{
+    return ((uint64_t) kLLTeamBytes / 8 / (2 * (uint64_t) (p < 1 ? 1 : p))) & ~uint64_t(1);  // whole items
+}
+__host__ __device__ constexpr uint64_t ll_capacity(int p) { return ll_sender_granules(p) * 4; }
+// The largest capacity (2 PEs): the cap of ISHMEM_LL_MAX_BYTES / set_param "ll_max_bytes", and
+// their default (no cap below the capacity).
+constexpr size_t kLLMaxBytes = ll_capacity(2);
+constexpr size_t kLLDefaultBytes = kLLMaxBytes;
 struct LLArgs {
     const char *src;
     char *dst;

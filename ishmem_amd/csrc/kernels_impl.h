@@ -1414,6 +1414,7 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
     const uint32_t ep = kernel_epoch(a);
     const uint64_t par = ep & 1u;
     const uint64_t tag = (uint64_t) ep << 32;
+    const uint64_t sg = ll_sender_granules(p);  // granules per (parity, sender) slot
     bool ok = true;
     for (uint64_t item = first; item < nitems; item += stride) {
         const uint64_t off = item * 8;
@@ -1421,7 +1422,7 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
         const uint64_t g0 = tag | (uint32_t) mine, g1 = tag | (uint32_t) (mine >> 32);
         for (int j = 0; j < p; ++j) {
             if (j == me) continue;
-            uint64_t *slot = a.peer_ring[j] + (par * kMaxPes + me) * kLLGranules + 2 * item;
+            uint64_t *slot = a.peer_ring[j] + (par * (uint64_t) p + me) * sg + 2 * item;
             __hip_atomic_store(slot, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(slot + 1, g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
@@ -1435,7 +1436,7 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
         for (int j = 0; j < p && ok; ++j) {
             uint64_t x = mine;
             if (j != me) {
-                const uint64_t *slot = a.my_ring + (par * kMaxPes + j) * kLLGranules + 2 * item;
+                const uint64_t *slot = a.my_ring + (par * (uint64_t) p + j) * sg + 2 * item;
                 uint64_t h0, h1;
                 for (;;) {
                     h0 = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -599,15 +599,16 @@ int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)
     return 0;
 }
 
-// Small payloads (<= ll_max_bytes, device memory anywhere, any element-aligned address — the
-// kernel picks 8-, 4- or 1-byte accesses, ll_load / ll_store): one-hop push of {data, epoch}
-// granules into the peers' rings, no barriers (ll_kernel).  The choice depends on the byte count
-// only, which every member shares.
+// Small payloads (<= the team's ring capacity, kernels.h ll_capacity, and <= ll_max_bytes; device
+// memory anywhere, any element-aligned address — the kernel picks 8-, 4- or 1-byte accesses,
+// ll_load / ll_store): one-hop push of {data, epoch} granules into the peers' rings, no barriers
+// (ll_kernel).  The choice depends on the byte count and the team size only, which every member
+// shares.
 bool ll_eligible(const State &s, const Team &t, const void *dst, const void *src, size_t bytes)
 {
     (void) dst;
     (void) src;
-    return t.size > 1 && bytes > 0 && (long long) bytes <= s.ll_max_bytes && bytes <= kLLMaxBytes;
+    return t.size > 1 && bytes > 0 && (long long) bytes <= s.ll_max_bytes && bytes <= ll_capacity(t.size);
 }
 
 // Collectives of one PE run in the order they were called, whatever streams they were enqueued
@@ -2754,6 +2755,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "oneshot_p2_max_bytes") return s.oneshot_p2;
     if (n == "phased_min_bytes") return s.phased_min == kPhasedOff ? -1 : s.phased_min;
     if (n == "ll_max_bytes") return s.ll_max_bytes;
+    if (n == "ll_capacity_bytes") return (long long) ll_capacity(s.npes);  // TEAM_WORLD's ring capacity
     if (n == "debug") return s.debug;
     if (n == "phased_peer_nt") return s.phased_peer_nt;
     if (n == "barrier_kind") return s.barrier_kind;

@@ -1066,7 +1066,8 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                         break
                 hip.stream_synchronize(occ)
                 done_iters += 1
-                kinds.add("ll" if n * es <= 65536 else ("big" if n * es > (1 << 20) else "mid"))
+                ll_cap = min(int(ish.get_param("ll_max_bytes")), (1 << 20) // len(members))  # kernels.h ll_capacity
+                kinds.add("ll" if n * es <= ll_cap else ("big" if n * es > (1 << 20) else "mid"))
                 occupied += occupier >= 0
             if pe == 0:
                 print(f"[stress] pe0: {done_iters}/{iters} iterations, {occupied} with an occupier, "

@@ -63,18 +63,24 @@ def run_pes(npes: int, scenarios: list[str], timeout: float = 240.0, env: dict |
     assert not allfails, "\n".join(allfails[:20])
 
 
+# ll=on: payloads <= 64 KiB take the one-hop granule path; cap: the default, up to the team's
+# ring capacity (1 MiB / team size: 512 KiB at 2 PEs, 349,520 B at 3, 256 KiB at 4); off: reduce-
+# scatter + all-gather for the same inputs.
+LL_ENV = {"on": 65536, "cap": None, "off": 0}
+
+
 @pytest.mark.parametrize("npes", [2, 4])
-@pytest.mark.parametrize("ll", ["on", "off"])
+@pytest.mark.parametrize("ll", ["on", "cap", "off"])
 def test_all_ops_types_vs_oracle_and_mpich_golden(npes, ll):
-    # ll=on: payloads <= 64 KiB take the one-hop granule path; ll=off forces reduce-scatter +
-    # all-gather for the same inputs.
-    run_pes(npes, ["golden"], env={"ISHMEM_LL_MAX_BYTES": 65536 if ll == "on" else 0})
+    run_pes(npes, ["golden"], env={"ISHMEM_LL_MAX_BYTES": LL_ENV[ll]})
 
 
 @pytest.mark.parametrize("npes", [2, 3])
-@pytest.mark.parametrize("ll", ["on", "off"])
+@pytest.mark.parametrize("ll", ["on", "cap", "off"])
 def test_inplace_offsets_edges(npes, ll):
-    run_pes(npes, ["inplace", "offsets", "offsets_large", "edge"], env={"ISHMEM_LL_MAX_BYTES": 65536 if ll == "on" else 0})
+    # offsets_large at 2 and 3 PEs: 70,001 floats (280 KB) and 262,147 bytes take the granule path
+    # only with ll=cap, from sources on another phase than dest, guard bytes checked.
+    run_pes(npes, ["inplace", "offsets", "offsets_large", "edge"], env={"ISHMEM_LL_MAX_BYTES": LL_ENV[ll]})
 
 
 def test_stream_staged_team():

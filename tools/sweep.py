@@ -51,7 +51,8 @@ def main() -> None:
         key = obj[0]
     if args.emulate_share1:
         os.environ["ISHMEM_TEST_PCI_BUS"] = f"fake-bus-{rank}"
-        os.environ["ISHMEM_AMD_LIB"] = str(Path(__file__).resolve().parents[1] / "ishmem_amd/libishmem_amd_testhooks.so")
+        # The test-hooks build unless an A/B variant (built with ISHMEMI_TEST_HOOKS) is named.
+        os.environ.setdefault("ISHMEM_AMD_LIB", str(Path(__file__).resolve().parents[1] / "ishmem_amd/libishmem_amd_testhooks.so"))
     import ishmem_amd as ish
     from ishmem_amd import hip
     dev = 0 if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else local
