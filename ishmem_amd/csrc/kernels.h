@@ -111,7 +111,15 @@ struct LLArgs {
     uint64_t timeout_ticks;
     uint32_t *ep_ctr;  // team's launch words (kEpTeamWords, see kEp*)
     int p, me;
+    // What the received items become (round 5; every member exchanges with every member in each
+    // mode, so no member can run more than one collective ahead of another):
+    //   kLLReduce - dest = fold of all p members' items;
+    //   kLLInscan / kLLExscan - dest = fold of members 0..me / 0..me-1 (sum; member 0's exclusive
+    //               result is 0);
+    //   kLLCollect - member j's bytes land at dest + j * nbytes (fcollect).
+    int mode;
 };
+constexpr int kLLReduce = 0, kLLInscan = 1, kLLExscan = 2, kLLCollect = 3;
 hipError_t launch_ll(int op, int dt, const LLArgs &a, hipStream_t s);
 
 // fcollect / collect (all-gather of the members' sources): member j's bytes land at

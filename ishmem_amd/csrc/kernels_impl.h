@@ -1391,9 +1391,8 @@ __device__ __forceinline__ uint64_t ll_load(const LLArgs &a, uint64_t off, uint6
     return mine;
 }
 
-__device__ __forceinline__ void ll_store(const LLArgs &a, uint64_t off, uint64_t valid, uint64_t v)
+__device__ __forceinline__ void ll_store(char *p, uint64_t valid, uint64_t v)
 {
-    char *p = a.dst + off;
     if (valid == 8 && ((uintptr_t) p & 7) == 0) {
         *(uint64_t *) p = v;
     } else if (valid == 8 && ((uintptr_t) p & 3) == 0) {
@@ -1428,11 +1427,13 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
         }
     }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    // Members folded: all (reduce), 0..me (inclusive scan), 0..me-1 (exclusive scan).
+    const int last = a.mode == kLLInscan ? me : a.mode == kLLExscan ? me - 1 : p - 1;
     for (uint64_t item = first; item < nitems && ok; item += stride) {
         const uint64_t off = item * 8;
         const uint64_t valid = a.nbytes - off < 8 ? a.nbytes - off : 8;
         const uint64_t mine = ll_load(a, off, valid);
-        uint64_t acc = 0;
+        uint64_t acc = 0;  // an empty fold (member 0's exclusive scan) stores zeros
         for (int j = 0; j < p && ok; ++j) {
             uint64_t x = mine;
             if (j != me) {
@@ -1451,9 +1452,10 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
                 }
                 x = (h0 & 0xffffffffull) | (h1 << 32);
             }
-            acc = (j == 0) ? x : fold8<T, OP>(acc, x);
+            if (a.mode == kLLCollect) ll_store(a.dst + (uint64_t) j * a.nbytes + off, valid, x);
+            else if (j <= last) acc = (j == 0) ? x : fold8<T, OP>(acc, x);
         }
-        if (ok) ll_store(a, off, valid, acc);
+        if (ok && a.mode != kLLCollect) ll_store(a.dst + off, valid, acc);
     }
     // *ret was zeroed by the caller: any thread that failed marks it (sticky over launches).
     if (!ok && a.ret) __hip_atomic_fetch_or(a.ret, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -697,8 +697,9 @@ int staging_release(State &s, hipStream_t st)
     return 0;
 }
 
+// mode: kernels.h kLLReduce / kLLInscan / kLLExscan / kLLCollect (what the received items become).
 int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, size_t bytes, int *ret,
-              hipStream_t st)
+              hipStream_t st, int mode = kLLReduce)
 {
     if (order_stream(s, st)) return 1;
     Team &t = s.teams[team];
@@ -719,6 +720,7 @@ int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, si
     a.ep_ctr = s.kern_ep + (size_t) kEpTeamWords * team;
     a.p = t.size;
     a.me = t.my_idx;
+    a.mode = mode;
     HIP_TRY(launch_ll(op, dt, a, st));
     return 0;
 }
@@ -1157,6 +1159,10 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
         if (staged < 0) staged = in_heap(s, src) ? 0 : 1;
         if (nbytes == 0) {
             if (team_sync_locked(s, team, st, ret)) return 1;
+        } else if (!staged && ll_eligible(s, t, dst, src, nbytes) && classify(s, dst) != Kind::Host) {
+            // Small payloads (round 5): the granule exchange, every member's bytes stored at their
+            // team-order offset (kLLCollect) — no start / done handshakes.
+            if (reduce_ll(s, team, ISHMEMI_OP_OR, ISHMEMI_DT_UINT8, dst, src, nbytes, ret, st, kLLCollect)) return 1;
         } else if (staged) {
             if (order_stream(s, st) || collect_staged(s, team, (char *) dst, (const char *) src, nb, ret, st)) return 1;
         } else if (collect_launch(s, team, dst, src, nb, ret, st)) {
@@ -1246,6 +1252,18 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
     } else {
         if (!in_heap(s, dst) || !in_heap(s, src)) return fail("scan: buffers must be symmetric-heap memory");
         if (((uintptr_t) dst | (uintptr_t) src) % es) return fail("scan: misaligned buffers");
+        if (ll_eligible(s, t, dst, src, n * es)) {
+            // Small payloads (round 5): the granule exchange, each member folding members 0..me
+            // (inclusive) or 0..me-1 (exclusive) — no scratch rows, no handshakes.
+            if (reduce_ll(s, team, ISHMEMI_OP_SUM, dt, dst, src, n * es, ret, st, inclusive ? kLLInscan : kLLExscan))
+                return 1;
+            if (mark_stream(s, st)) return 1;
+            if (blocking) {
+                HIP_TRY(hipStreamSynchronize(st));
+                if (check_team_errors(s, team)) return 1;
+            }
+            return 0;
+        }
         // Segments whose p scratch rows fit the staging region (member c's rows: [k][chunk c]).
         const uint64_t ipc_max = ((s.staging_bytes / es) / (uint64_t) t.size) & ~uint64_t(63);
         const uint64_t seg = ipc_max * (uint64_t) t.size;

@@ -96,9 +96,12 @@ def test_huge_2p5GiB_per_pe_head_tail_and_2GiB_boundary():
 
 
 @pytest.mark.parametrize("npes", [2, 3, 4])
-def test_fcollect_collect_scan_vs_tester_patterns_and_oracle(npes):
-    # Small staging region so the scan's segment loop runs several times.
-    run_pes(npes, ["collect", "scan"], env={"ISHMEM_STAGING_SIZE": "4M"}, timeout=300)
+@pytest.mark.parametrize("ll", ["cap", "off"])
+def test_fcollect_collect_scan_vs_tester_patterns_and_oracle(npes, ll):
+    # Small staging region so the scan's segment loop runs several times.  ll=cap (the default):
+    # fcollect and scans up to the granule ring's capacity take the granule exchange (kLLCollect /
+    # kLLInscan / kLLExscan); off: the handshake kernels for every size.
+    run_pes(npes, ["collect", "scan"], env={"ISHMEM_STAGING_SIZE": "4M", "ISHMEM_LL_MAX_BYTES": LL_ENV[ll]}, timeout=300)
 
 
 @pytest.mark.parametrize("npes", [2, 3])
@@ -106,8 +109,8 @@ def test_scan_collect_on_the_phased_paths(npes):
     # The threshold forced to 0: at 2 PEs disjoint scans take the direct fold (no scratch), in-place
     # ones and every scan at 3 PEs the phased segments; fcollect / collect the phased pull grid.
     # Tester patterns and seeded inputs vs the oracle, as in the default-path test above.
-    run_pes(npes, ["collect", "scan"], env={"ISHMEM_STAGING_SIZE": "4M", "ISHMEM_PHASED_MIN_BYTES": 0},
-            timeout=300)
+    run_pes(npes, ["collect", "scan"], env={"ISHMEM_STAGING_SIZE": "4M", "ISHMEM_PHASED_MIN_BYTES": 0,
+                                            "ISHMEM_LL_MAX_BYTES": 0}, timeout=300)
 
 
 def test_launch_parameters_agreed_at_init():
