@@ -84,11 +84,12 @@ struct ReduceArgs {
 // Small-message ("LL") path: 8-byte granules {4 data bytes | 32-bit epoch} pushed into every
 // peer's fine-grained receive ring.  One ring of kLLTeamBytes per team, laid out by the team's size
 // p as [parity 2][sender p][ll_sender_granules(p)] u64, so a sender's capacity is
-// kLLTeamBytes / (4p) payload bytes: 512 KiB at 2 PEs, 256 KiB at 4, 128 KiB at 8, 64 KiB at 16.
-// The path's link traffic is 2(p-1)·B per PE, and its crossover with the persistent kernel,
-// measured, falls as 1/p as well: the capacity is the default threshold.
+// kLLTeamBytes / (4p) payload bytes: 1 MiB at 2 PEs, 512 KiB at 4, 256 KiB at 8, 128 KiB at 16.
+// The default threshold is the smaller of that and kLLDefaultBytes (512 KiB): measured against the
+// persistent kernel, the granule path wins up to 512 KiB at 2 and 4 PEs and loses at 1 MiB
+// (DESIGN.md §3, round 5); its link traffic, 2(p-1)·B per PE, grows with p as the capacity shrinks.
 #ifndef ISHMEMI_LL_TEAM_BYTES
-#define ISHMEMI_LL_TEAM_BYTES (4u << 20)
+#define ISHMEMI_LL_TEAM_BYTES (8u << 20)
 #endif
 constexpr size_t kLLTeamBytes = ISHMEMI_LL_TEAM_BYTES;
 __host__ __device__ constexpr uint64_t ll_sender_granules(int p)
@@ -96,10 +97,10 @@ __host__ __device__ constexpr uint64_t ll_sender_granules(int p)
     return ((uint64_t) kLLTeamBytes / 8 / (2 * (uint64_t) (p < 1 ? 1 : p))) & ~uint64_t(1);  // whole items
 }
 __host__ __device__ constexpr uint64_t ll_capacity(int p) { return ll_sender_granules(p) * 4; }
-// The largest capacity (2 PEs): the cap of ISHMEM_LL_MAX_BYTES / set_param "ll_max_bytes", and
-// their default (no cap below the capacity).
+// The largest capacity (2 PEs) caps ISHMEM_LL_MAX_BYTES / set_param "ll_max_bytes"; their default
+// is kLLDefaultBytes.
 constexpr size_t kLLMaxBytes = ll_capacity(2);
-constexpr size_t kLLDefaultBytes = kLLMaxBytes;
+constexpr size_t kLLDefaultBytes = 512u << 10;
 struct LLArgs {
     const char *src;
     char *dst;
@@ -271,6 +272,13 @@ int realign_grid_cap();
 // "collect_realign", A/B only) keeps the narrow 4- / 1-byte items.
 void set_collect_realign(int on);
 int collect_realign();
+// The phased reduce-scatter with sources on another 16-B phase than dest (set_param
+// "phase_unaligned", default 1): rs_phase_kernel with unaligned 16-B source loads (the hardware
+// splits a load that crosses a line); 0 = rs_phase_realign_kernel (aligned loads, DPP + LDS
+// realign).  2 PEs x 1 GiB on one GPU, source 4 B off: reduce-scatter grid 0.525-0.528 vs
+// 0.556-0.563 ms; 4 PEs 0.920-0.922 vs 0.932-0.945 (profiles/r05/phase_unaligned/).
+void set_phase_unaligned(int on);
+int phase_unaligned();
 // Test hook: `grid` workgroups that each hold half a CU (1024 work-items, 80 KiB LDS) for `usec`.
 hipError_t launch_occupy(int grid, uint64_t usec, hipStream_t s);
 hipError_t launch_produce_u32(uint32_t *dst, const uint32_t *a, const uint32_t *b, uint64_t n, hipStream_t s);

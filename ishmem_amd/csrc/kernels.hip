@@ -18,6 +18,9 @@ int realign_grid_cap() { return g_realign_grid_cap; }
 int g_collect_realign = 1;
 void set_collect_realign(int on) { g_collect_realign = on != 0; }
 int collect_realign() { return g_collect_realign; }
+int g_phase_unaligned = 1;
+void set_phase_unaligned(int on) { g_phase_unaligned = on != 0; }
+int phase_unaligned() { return g_phase_unaligned; }
 
 #define ISHMEMI_DECL_OP(N)                                                                         \
     hipError_t launch_allreduce_op##N(int dt, bool vec, const ReduceArgs &a, int grid,             \

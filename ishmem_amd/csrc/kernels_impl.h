@@ -1336,7 +1336,7 @@ hipError_t rs_phase_t(const PhaseArgs &a, hipStream_t s)
     auto go = [&](auto kernel) {
         hipLaunchKernelGGL(kernel, dim3(phase_grid(kernel, len)), dim3(kFaninBlock), 0, s, a);
     };
-    if (a.shift) {
+    if (a.shift && !phase_unaligned()) {
         uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((len + kRsRealignBlock - 1) / kRsRealignBlock,
                                                               (1ull << 31) / kRsRealignBlock));
         if (realign_grid_cap() > 0) g = std::min<uint64_t>(g, (uint64_t) realign_grid_cap());

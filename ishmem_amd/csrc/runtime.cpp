@@ -1159,9 +1159,12 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
         if (staged < 0) staged = in_heap(s, src) ? 0 : 1;
         if (nbytes == 0) {
             if (team_sync_locked(s, team, st, ret)) return 1;
-        } else if (!staged && ll_eligible(s, t, dst, src, nbytes) && classify(s, dst) != Kind::Host) {
+        } else if (!staged && ll_eligible(s, t, dst, src, nbytes) && 2 * nbytes <= ll_capacity(t.size) &&
+                   classify(s, dst) != Kind::Host) {
             // Small payloads (round 5): the granule exchange, every member's bytes stored at their
-            // team-order offset (kLLCollect) — no start / done handshakes.
+            // team-order offset (kLLCollect) — no start / done handshakes.  Up to half the ring's
+            // capacity: the pull kernel moves (p-1)·B where the granules move 2(p-1)·B, and at
+            // 4 PEs x 256 KiB the two were already within 8 % (profiles/r05/ll_coll/).
             if (reduce_ll(s, team, ISHMEMI_OP_OR, ISHMEMI_DT_UINT8, dst, src, nbytes, ret, st, kLLCollect)) return 1;
         } else if (staged) {
             if (order_stream(s, st) || collect_staged(s, team, (char *) dst, (const char *) src, nb, ret, st)) return 1;
@@ -2735,6 +2738,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "realign_grid_cap") set_realign_grid_cap((int) std::min<long long>(std::max<long long>(value, 0), 1 << 30));
     else if (n == "collect_realign") set_collect_realign((int) (value != 0));
     else if (n == "ar_shifted") s.ar_shifted = value != 0;  // measurement: set alike on every PE
+    else if (n == "phase_unaligned") set_phase_unaligned((int) (value != 0));
     else if (n == "stream_barrier_release") {
         // Escape hatch of the stream barrier, which has no timeout (team_barrier): store the team's
         // latest stream-barrier epoch into every slot of this PE's own wait row, so a stream stuck
@@ -2780,6 +2784,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "realign_grid_cap") return realign_grid_cap();
     if (n == "collect_realign") return collect_realign();
     if (n == "ar_shifted") return s.ar_shifted;
+    if (n == "phase_unaligned") return phase_unaligned();
     if (n == "flags_fine_grained") return s.flags_kind != kFlagsCoarse ? 1 : 0;
     if (n == "flags_kind") return s.flags_kind;
     if (n == "staging_bytes") return (long long) s.staging_bytes;

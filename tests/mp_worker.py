@@ -93,6 +93,8 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             # Tests only: at most 3 workgroups for the realigned kernels, so the realigned
             # reduce-scatter's grid-stride loop (edge[] reuse between passes) runs at test sizes.
             ish.set_param("realign_grid_cap", 3)
+            # ... and the realigning reduce-scatter kernel (not the default unaligned-load one).
+            ish.set_param("phase_unaligned", 0)
 
         if "sbrelease" in scenarios:
             # The stream barrier's escape hatch (set_param "stream_barrier_release"): PE 0 enters a
