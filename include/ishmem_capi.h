@@ -266,8 +266,9 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
 
 /* ---- diagnostics / parameters ----------------------------------------------------------------
  * ishmemi_c_set_param names: "max_blocks" (workgroups per collective launch, <= 1024),
- * "ll_max_bytes" (cap on the one-hop granule path, <= 524288; the path also stops at the team's
- * ring capacity, 1 MiB / team size: get_param "ll_capacity_bytes" for TEAM_WORLD), "timeout_ms" (bound on every
+ * "ll_max_bytes" (cap on the one-hop granule path, default 524288, <= 1048576; the path also stops
+ * at the team's ring capacity, 2 MiB / team size: get_param "ll_capacity_bytes" for TEAM_WORLD),
+ * "timeout_ms" (bound on every
  * device-side spin), "stream_order" (1: collectives issued on different streams are ordered by
  * the library in call order, ~2 us per call; 0, the default: the caller orders them, as the
  * reference requires), "oneshot_p2_max_bytes" (two-member teams: one-phase fold up to this size,
