@@ -989,6 +989,68 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 ish.ishmem_free(b_)
             ish.set_param("max_blocks", int(os.environ.get("ISHMEM_MAX_BLOCKS", 1024)))
 
+        if "llchain" in scenarios:
+            # Granule-path collectives back to back on one stream with no host synchronisation
+            # (round 5: reduce, fcollect, inclusive / exclusive scan share the rings, whose two
+            # parities alternate by epoch): 32 calls of random kind and size up to the granule
+            # threshold, each with its own source and dest, PEs enqueueing with random host delays
+            # so the device-side skew varies; every dest then checked against the oracle.
+            import time as _t
+            rng = np.random.default_rng(4242)
+            cap = min(int(ish.get_param("ll_max_bytes")), int(ish.get_param("ll_capacity_bytes")))
+            K = 32
+            plan = []
+            for k in range(K):
+                kind = ["reduce", "fcollect", "inscan", "exscan"][int(rng.integers(4))]
+                dt = [DT["int32"], DT["float"], DT["uint64"], DT["double"]][int(rng.integers(4))]
+                es = np.dtype(oracle.NP[dt]).itemsize
+                limit = cap // 2 if kind == "fcollect" else cap
+                n = max(1, int(np.exp(rng.uniform(0.0, np.log(limit // es)))))
+                op = OPS["sum"] if kind != "reduce" else [OPS["sum"], OPS["max"], OPS["min"]][int(rng.integers(3))]
+                plan.append((kind, dt, es, n, op))
+            bufs = []
+            for k, (kind, dt, es, n, op) in enumerate(plan):
+                ins = [oracle.fill_random(dt, 9000 + 31 * k + j, n) for j in range(npes)]
+                sb = ish.ishmem_malloc(n * es)
+                db = ish.ishmem_malloc(n * es * (npes if kind == "fcollect" else 1))
+                hip.upload(sb, ins[pe])
+                bufs.append((sb, db, ins))
+            st_c = hip.stream_create()
+            ret_c = ish.ishmem_malloc(4)
+            hip.memset(ret_c, 0, 4)
+            ish.ishmem_barrier_all()
+            delays = np.random.default_rng(77 + pe).uniform(0, 2e-4, K)
+            for k, (kind, dt, es, n, op) in enumerate(plan):
+                _t.sleep(float(delays[k]))
+                sb, db, _ = bufs[k]
+                if kind == "reduce":
+                    r = ish.reduce_on_stream(ONAMES[op], NAMES[dt], db, sb, n, ret_c, st_c)
+                elif kind == "fcollect":
+                    r = ish.fcollect_on_stream(db, sb, n * es, ret_c, st_c)
+                else:
+                    r = ish.lib().ishmemi_c_scan_on_stream(0, dt, 1 if kind == "inscan" else 0, db, sb, n, ret_c, st_c)
+                if r:
+                    fails.append(f"pe{pe} llchain k={k} {kind}: rc={r} {ish.last_error()}")
+                    break
+            hip.stream_synchronize(st_c)
+            if int(hip.download(ret_c, 1, np.int32)[0]) != 0:
+                fails.append(f"pe{pe} llchain: *ret set")
+            for k, (kind, dt, es, n, op) in enumerate(plan):
+                sb, db, ins = bufs[k]
+                tag = f"llchain k={k} {kind} dt={NAMES[dt]} n={n}"
+                if kind == "reduce":
+                    check(tag, op, dt, ins, hip.download(db, n, oracle.NP[dt]))
+                elif kind == "fcollect":
+                    if not _bits_equal(hip.download(db, n * npes, oracle.NP[dt]), np.concatenate(ins)):
+                        fails.append(f"pe{pe} {tag} wrong")
+                else:
+                    if not _bits_equal(hip.download(db, n, oracle.NP[dt]), oracle.scan_fold(dt, ins, pe, kind == "inscan")):
+                        fails.append(f"pe{pe} {tag} wrong")
+                ish.ishmem_free(db)
+                ish.ishmem_free(sb)
+            ish.ishmem_free(ret_c)
+            hip.stream_destroy(st_c)
+
         if "stress" in scenarios:
             # Randomised protocol stress: every iteration draws (same draw on every PE) an
             # (op, type), a length from 1 element to 4 Mi (log-uniform: granule path, one-shot,

@@ -95,6 +95,13 @@ def test_huge_2p5GiB_per_pe_head_tail_and_2GiB_boundary():
     run_pes(2, ["huge"], env={"ISHMEM_MAX_BLOCKS": 64, "ISHMEM_SYMMETRIC_SIZE": "6G"}, timeout=400)
 
 
+@pytest.mark.parametrize("npes", [2, 3, 4, 8])
+def test_granule_collectives_chained_without_sync(npes):
+    # 32 granule-path reduces / fcollects / scans back to back on one stream, random sizes up to
+    # the threshold, random host delays per PE: the rings' parity alternation across modes.
+    run_pes(npes, ["llchain"], timeout=200)
+
+
 @pytest.mark.parametrize("npes", [2, 3, 4])
 @pytest.mark.parametrize("ll", ["cap", "off"])
 def test_fcollect_collect_scan_vs_tester_patterns_and_oracle(npes, ll):
