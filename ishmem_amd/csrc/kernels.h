@@ -94,7 +94,20 @@ struct ReduceArgs {
 constexpr size_t kLLTeamBytes = ISHMEMI_LL_TEAM_BYTES;
 __host__ __device__ constexpr uint64_t ll_sender_granules(int p)
 {
-    return ((uint64_t) kLLTeamBytes / 8 / (2 * (uint64_t) (p < 1 ? 1 : p))) & ~uint64_t(1);  // whole items
+    // Whole blocks of 64 items (128 granules: ll_granule below).
+    return ((uint64_t) kLLTeamBytes / 8 / (2 * (uint64_t) (p < 1 ? 1 : p))) & ~uint64_t(127);
+}
+// Granule index of item `item`'s half h (0: low 4 bytes, 1: high) in a sender's slot.  Items are
+// grouped by 64 (one wave's lanes): [low halves of items 64b .. 64b+63][their high halves], so each
+// of a wave's two granule stores (and polls) covers 512 contiguous bytes, whole 64-B lines of the
+// uncached ring, instead of every other 8 B of 1 KiB.  ISHMEMI_LL_PAIRED=1 keeps the round-4
+// layout (item i at granules 2i, 2i + 1; A/B builds only).
+#ifndef ISHMEMI_LL_PAIRED
+#define ISHMEMI_LL_PAIRED 0
+#endif
+__host__ __device__ constexpr uint64_t ll_granule(uint64_t item, int h)
+{
+    return ISHMEMI_LL_PAIRED ? 2 * item + (uint64_t) h : (item & ~uint64_t(63)) * 2 + (uint64_t) h * 64 + (item & 63);
 }
 __host__ __device__ constexpr uint64_t ll_capacity(int p) { return ll_sender_granules(p) * 4; }
 // The largest capacity (2 PEs) caps ISHMEM_LL_MAX_BYTES / set_param "ll_max_bytes"; their default

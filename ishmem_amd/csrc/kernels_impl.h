@@ -1421,9 +1421,9 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
         const uint64_t g0 = tag | (uint32_t) mine, g1 = tag | (uint32_t) (mine >> 32);
         for (int j = 0; j < p; ++j) {
             if (j == me) continue;
-            uint64_t *slot = a.peer_ring[j] + (par * (uint64_t) p + me) * sg + 2 * item;
-            __hip_atomic_store(slot, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(slot + 1, g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            uint64_t *slot = a.peer_ring[j] + (par * (uint64_t) p + me) * sg;
+            __hip_atomic_store(slot + ll_granule(item, 0), g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(slot + ll_granule(item, 1), g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -1437,11 +1437,11 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
         for (int j = 0; j < p && ok; ++j) {
             uint64_t x = mine;
             if (j != me) {
-                const uint64_t *slot = a.my_ring + (par * (uint64_t) p + j) * sg + 2 * item;
+                const uint64_t *slot = a.my_ring + (par * (uint64_t) p + j) * sg;
                 uint64_t h0, h1;
                 for (;;) {
-                    h0 = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    h1 = __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    h0 = __hip_atomic_load(slot + ll_granule(item, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    h1 = __hip_atomic_load(slot + ll_granule(item, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     if ((h0 >> 32) == ep && (h1 >> 32) == ep) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
                         ok = false;
