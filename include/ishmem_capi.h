@@ -275,7 +275,12 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
  * default 64 MiB), "phased_min_bytes" (payloads of at least this size take the phased path:
  * barrier, one-shot reduce-scatter, barrier, one-shot all-gather, barrier; -1 disables it),
  * "phase_events" (1: the next phased reduces record HIP events between their five launches, read
- * with ishmemi_c_phase_times; a measurement hook), "debug".  "ll_max_bytes",
+ * with ishmemi_c_phase_times; a measurement hook), "debug"; A/B switches for measurements, set
+ * alike on every PE: "ar_shifted" (1, default: the persistent kernel keeps 16-B items for sources on
+ * another 16-B phase than dest, read with unaligned loads; 0: element-granular), "phase_unaligned"
+ * (1, default: the phased reduce-scatter reads such sources with unaligned 16-B loads; 0: the
+ * realigning kernel), "collect_realign" (1, default: collect members off the 16-B grid realigned;
+ * 0: narrow items), "barrier_kind" (0 kernel, 1 stream memory operations).  "ll_max_bytes",
  * "oneshot_p2_max_bytes" and "phased_min_bytes" choose the kernels of a multi-PE call: init
  * agrees on them (the minimum over the PEs; the maximum for "phased_min_bytes") and a later
  * set_param must be made with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,
