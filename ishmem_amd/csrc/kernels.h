@@ -130,10 +130,13 @@ struct LLArgs {
     //   kLLReduce - dest = fold of all p members' items;
     //   kLLInscan / kLLExscan - dest = fold of members 0..me / 0..me-1 (sum; member 0's exclusive
     //               result is 0);
-    //   kLLCollect - member j's bytes land at dest + j * nbytes (fcollect).
+    //   kLLCollect - member j's bytes land at dest + j * nbytes (fcollect);
+    //   kLLBroadcast - member `root`'s bytes land at every member's dest; the others push one
+    //               token item (no source read) so every member still hears from every member.
     int mode;
+    int root;
 };
-constexpr int kLLReduce = 0, kLLInscan = 1, kLLExscan = 2, kLLCollect = 3;
+constexpr int kLLReduce = 0, kLLInscan = 1, kLLExscan = 2, kLLCollect = 3, kLLBroadcast = 4;
 hipError_t launch_ll(int op, int dt, const LLArgs &a, hipStream_t s);
 
 // fcollect / collect (all-gather of the members' sources): member j's bytes land at

@@ -1414,10 +1414,13 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
     const uint64_t par = ep & 1u;
     const uint64_t tag = (uint64_t) ep << 32;
     const uint64_t sg = ll_sender_granules(p);  // granules per (parity, sender) slot
+    const bool bcast = a.mode == kLLBroadcast;
+    const bool has_src = !bcast || me == a.root;  // a broadcast's non-roots read no source
     bool ok = true;
     for (uint64_t item = first; item < nitems; item += stride) {
+        if (!has_src && item != 0) break;  // non-root: the item-0 token only
         const uint64_t off = item * 8;
-        const uint64_t mine = ll_load(a, off, a.nbytes - off < 8 ? a.nbytes - off : 8);
+        const uint64_t mine = has_src ? ll_load(a, off, a.nbytes - off < 8 ? a.nbytes - off : 8) : 0;
         const uint64_t g0 = tag | (uint32_t) mine, g1 = tag | (uint32_t) (mine >> 32);
         for (int j = 0; j < p; ++j) {
             if (j == me) continue;
@@ -1432,9 +1435,11 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
     for (uint64_t item = first; item < nitems && ok; item += stride) {
         const uint64_t off = item * 8;
         const uint64_t valid = a.nbytes - off < 8 ? a.nbytes - off : 8;
-        const uint64_t mine = ll_load(a, off, valid);
+        const uint64_t mine = has_src ? ll_load(a, off, valid) : 0;
         uint64_t acc = 0;  // an empty fold (member 0's exclusive scan) stores zeros
         for (int j = 0; j < p && ok; ++j) {
+            // Broadcast: the root's items, plus every member's item-0 token.
+            if (bcast && j != a.root && j != me && item != 0) continue;
             uint64_t x = mine;
             if (j != me) {
                 const uint64_t *slot = a.my_ring + (par * (uint64_t) p + j) * sg;
@@ -1453,9 +1458,10 @@ __global__ __launch_bounds__(kBlock) void ll_kernel(LLArgs a)
                 x = (h0 & 0xffffffffull) | (h1 << 32);
             }
             if (a.mode == kLLCollect) ll_store(a.dst + (uint64_t) j * a.nbytes + off, valid, x);
+            else if (bcast) { if (j == a.root) ll_store(a.dst + off, valid, x); }
             else if (j <= last) acc = (j == 0) ? x : fold8<T, OP>(acc, x);
         }
-        if (ok && a.mode != kLLCollect) ll_store(a.dst + off, valid, acc);
+        if (ok && a.mode != kLLCollect && !bcast) ll_store(a.dst + off, valid, acc);
     }
     // *ret was zeroed by the caller: any thread that failed marks it (sticky over launches).
     if (!ok && a.ret) __hip_atomic_fetch_or(a.ret, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -699,7 +699,7 @@ int staging_release(State &s, hipStream_t st)
 
 // mode: kernels.h kLLReduce / kLLInscan / kLLExscan / kLLCollect (what the received items become).
 int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, size_t bytes, int *ret,
-              hipStream_t st, int mode = kLLReduce)
+              hipStream_t st, int mode = kLLReduce, int root = 0)
 {
     if (order_stream(s, st)) return 1;
     Team &t = s.teams[team];
@@ -721,6 +721,7 @@ int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, si
     a.p = t.size;
     a.me = t.my_idx;
     a.mode = mode;
+    a.root = root;
     HIP_TRY(launch_ll(op, dt, a, st));
     return 0;
 }
@@ -1185,6 +1186,7 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
 // anything that must match across members is launched (a member that failed alone would leave
 // its peers waiting for launches that never come).  Called without the state lock.
 constexpr uint64_t kAgreeStaged = 1ull << 62, kAgreeFail = 1ull << 63;
+constexpr uint64_t kAgreeDestOffHeap = 1ull << 61;  // broadcast: this member's dest is not in the heap
 bool member_call(const State &s, int team);
 
 // The agreement step of the blocking fcollect / collect / scan / broadcast (staged path, counts,
@@ -2639,6 +2641,13 @@ int ishmemi_c_broadcast_on_stream(int team, void *dest, const void *source, size
     if (nbytes == 0) return team_sync_locked(s, team, st, ret) || mark_stream(s, st);
     if (!in_heap(s, source)) return fail("broadcast_on_stream: source must be symmetric-heap memory");
     if (!device_writable(s, dest)) return fail("broadcast_on_stream: dest must be heap, device or pinned host memory");
+    if (in_heap(s, dest) && ll_eligible(s, t, dest, source, nbytes) && 2 * nbytes <= ll_capacity(t.size)) {
+        // Small payloads (round 5): the root's bytes as granules into every member's ring, the
+        // others one token each (kLLBroadcast) — no handshakes.  Symmetric dest: every member
+        // decides alike.
+        if (reduce_ll(s, team, ISHMEMI_OP_OR, ISHMEMI_DT_UINT8, dest, source, nbytes, ret, st, kLLBroadcast, root)) return 1;
+        return mark_stream(s, st);
+    }
     uint64_t counts[kMaxPes] = {}, zero[kMaxPes] = {};
     counts[root] = nbytes;
     const char *srcs[kMaxPes];
@@ -2668,6 +2677,7 @@ int ishmemi_c_broadcast(int team, void *dest, const void *source, size_t nbytes,
     uint64_t mine = 0;
     if (me_root) mine = in_heap(s, source) ? (uint64_t) ((const char *) source - s.heap) : kAgreeStaged;
     if (nbytes && !device_writable(s, dest)) mine |= kAgreeFail;
+    if (!in_heap(s, dest)) mine |= kAgreeDestOffHeap;
     uint64_t all[kMaxPes], any = 0;
     if (team_exchange(team, mine, all)) return 1;
     for (int j = 0; j < p; ++j) any |= all[j];
@@ -2676,13 +2686,19 @@ int ishmemi_c_broadcast(int team, void *dest, const void *source, size_t nbytes,
     uint64_t counts[kMaxPes] = {}, zero[kMaxPes] = {};
     counts[root] = nbytes;
     std::lock_guard<std::mutex> lk(s.mu);
-    if (all[root] & kAgreeStaged) {
+    if (!(all[root] & kAgreeStaged) && !(any & kAgreeDestOffHeap) && ll_eligible(s, t, dest, source, nbytes) &&
+        2 * nbytes <= ll_capacity(p)) {
+        // Small payloads, every dest in the heap (agreed above): the granule broadcast
+        // (kLLBroadcast); the root reads its own source, the others none.
+        if (reduce_ll(s, team, ISHMEMI_OP_OR, ISHMEMI_DT_UINT8, dest, source, nbytes, nullptr, 0, kLLBroadcast, root))
+            return 1;
+    } else if (all[root] & kAgreeStaged) {
         if (order_stream(s, 0) || collect_staged(s, team, (char *) dest, (const char *) source, counts, nullptr, 0))
             return 1;
     } else {
         const char *srcs[kMaxPes];
         const int groot = t.start + root * t.stride;
-        for (int j = 0; j < p; ++j) srcs[j] = s.peer_heap[groot] + all[root];
+        for (int j = 0; j < p; ++j) srcs[j] = s.peer_heap[groot] + (all[root] & ~kAgreeDestOffHeap);
         if (collect_launch(s, team, dest, nullptr, counts, nullptr, 0, zero, srcs)) return 1;
     }
     if (mark_stream(s, 0)) return 1;

@@ -991,7 +991,7 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
 
         if "llchain" in scenarios:
             # Granule-path collectives back to back on one stream with no host synchronisation
-            # (round 5: reduce, fcollect, inclusive / exclusive scan share the rings, whose two
+            # (round 5: reduce, fcollect, inclusive / exclusive scan, broadcast share the rings, whose two
             # parities alternate by epoch): 32 calls of random kind and size up to the granule
             # threshold, each with its own source and dest, PEs enqueueing with random host delays
             # so the device-side skew varies; every dest then checked against the oracle.
@@ -1001,12 +1001,14 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             K = 32
             plan = []
             for k in range(K):
-                kind = ["reduce", "fcollect", "inscan", "exscan"][int(rng.integers(4))]
+                kind = ["reduce", "fcollect", "inscan", "exscan", "broadcast"][int(rng.integers(5))]
                 dt = [DT["int32"], DT["float"], DT["uint64"], DT["double"]][int(rng.integers(4))]
                 es = np.dtype(oracle.NP[dt]).itemsize
-                limit = cap // 2 if kind == "fcollect" else cap
+                limit = cap // 2 if kind in ("fcollect", "broadcast") else cap
                 n = max(1, int(np.exp(rng.uniform(0.0, np.log(limit // es)))))
                 op = OPS["sum"] if kind != "reduce" else [OPS["sum"], OPS["max"], OPS["min"]][int(rng.integers(3))]
+                if kind == "broadcast":
+                    op = int(rng.integers(npes))  # the root
                 plan.append((kind, dt, es, n, op))
             bufs = []
             for k, (kind, dt, es, n, op) in enumerate(plan):
@@ -1027,6 +1029,8 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                     r = ish.reduce_on_stream(ONAMES[op], NAMES[dt], db, sb, n, ret_c, st_c)
                 elif kind == "fcollect":
                     r = ish.fcollect_on_stream(db, sb, n * es, ret_c, st_c)
+                elif kind == "broadcast":
+                    r = ish.broadcast_on_stream(db, sb, n * es, op, ret_c, st_c)
                 else:
                     r = ish.lib().ishmemi_c_scan_on_stream(0, dt, 1 if kind == "inscan" else 0, db, sb, n, ret_c, st_c)
                 if r:
@@ -1043,6 +1047,9 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 elif kind == "fcollect":
                     if not _bits_equal(hip.download(db, n * npes, oracle.NP[dt]), np.concatenate(ins)):
                         fails.append(f"pe{pe} {tag} wrong")
+                elif kind == "broadcast":
+                    if not _bits_equal(hip.download(db, n, oracle.NP[dt]), ins[op]):
+                        fails.append(f"pe{pe} {tag} root={op} wrong")
                 else:
                     if not _bits_equal(hip.download(db, n, oracle.NP[dt]), oracle.scan_fold(dt, ins, pe, kind == "inscan")):
                         fails.append(f"pe{pe} {tag} wrong")

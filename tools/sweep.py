@@ -23,7 +23,7 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--min-bytes", type=int, default=4)
     ap.add_argument("--factor", type=int, default=4)
-    ap.add_argument("--coll", choices=["reduce", "fcollect", "inscan"], default="reduce")
+    ap.add_argument("--coll", choices=["reduce", "fcollect", "inscan", "broadcast"], default="reduce")
     ap.add_argument("--graph", action="store_true", help="time a hipGraph of --iters captured calls")
     ap.add_argument("--blocking", action="store_true",
                     help="blocking host calls (ishmem_fcollectmem / ishmem_float_sum_inscan / ishmem_float_sum_reduce), "
@@ -75,11 +75,15 @@ def main() -> None:
         if args.blocking:
             if args.coll == "fcollect":
                 return ish.ishmem_fcollectmem(dst, src, n * 4)
+            if args.coll == "broadcast":
+                return ish.ishmem_broadcastmem(dst, src, n * 4, 0)
             if args.coll == "inscan":
                 return ish.lib().ishmemi_c_scan(0, ish.DTYPES["float"], 1, dst, src, n)
             return ish.ishmem_float_sum_reduce(dst, src, n)
         if args.coll == "fcollect":
             return ish.fcollect_on_stream(dst, src, n * 4, 0, st)
+        if args.coll == "broadcast":
+            return ish.broadcast_on_stream(dst, src, n * 4, 0, 0, st)
         if args.coll == "inscan":
             return ish.lib().ishmemi_c_scan_on_stream(0, ish.DTYPES["float"], 1, dst, src, n, None, st)
         return ish.ishmemx_float_sum_reduce_on_stream(dst + 4 * do, src + 4 * so, n, 0, st)
@@ -89,6 +93,8 @@ def main() -> None:
         base = (i % 1024).astype(np.float32)
         if args.coll == "fcollect":  # the last k elements of the dest = PE world-1's tail
             return base + np.float32(world - 1)
+        if args.coll == "broadcast":  # root 0's source
+            return base
         if args.coll == "inscan":
             return base * (rank + 1) + np.float32(rank * (rank + 1) / 2)
         return base * world + np.float32(world * (world - 1) / 2)
