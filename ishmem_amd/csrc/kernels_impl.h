@@ -24,13 +24,17 @@
 //   * rs_phase_kernel / ag_phase_kernel: the same reduce-scatter + all-gather for large payloads
 //     as two one-shot grids (the fan-in kernel's shape) between one-workgroup team barriers —
 //     nothing in either grid waits, so it runs at the streaming kernels' rate (round 3).
+//   * ll_kernel: small payloads (up to 512 KiB, 2 MiB / p) with no handshake at all: every member
+//     pushes its bytes as {4 B data, 32-bit epoch} granules into every peer's ring and folds what
+//     it receives; the same exchange carries small fcollect, sum scans and broadcasts (round 5).
 //   * The barriers replace ishmemi_team_sync's psync counters (src/collectives/sync_impl.h:30-69)
 //     with epoch-tagged flags in fine-grained memory: one "started" flag per member, one
 //     "ready" flag per reduced segment (the RS -> AG hand-off) and one "done reading" flag per
 //     member, exchanged by whichever workgroup gets there; work is grabbed from per-launch
 //     counters, so no workgroup ever waits for a particular peer workgroup and the launch
-//     completes whatever part of the grid is resident.  All remote data accesses are LOADS
-//     (pull), so no PE's L2 can hold stale copies of bytes a peer wrote.
+//     completes whatever part of the grid is resident.  All remote payload accesses outside the
+//     granule rings are LOADS (pull), so no PE's L2 can hold stale copies of bytes a peer wrote;
+//     the rings are uncached fine-grained memory written and polled with system-scope atomics.
 #pragma once
 #include <algorithm>
 #include <map>
