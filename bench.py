@@ -115,9 +115,12 @@ def pmc_traffic(kernel_tag: str, nbytes: int):
     return None
 
 
-def multi_pe_kernel(B: int, phased_min: int) -> str:
-    """The multi-PE kernels a B-byte f32 sum takes (runtime.cpp reduce_heap): the phased path's
-    one-shot grids for payloads of at least phased_min bytes (-1: off), else the persistent kernel."""
+def multi_pe_kernel(B: int, phased_min: int, world: int = 0, oneshot_p2: int = -1) -> str:
+    """The multi-PE kernels a B-byte f32 sum with disjoint buffers takes (runtime.cpp reduce_heap):
+    two members up to oneshot_p2 bytes fold the whole array between two barriers; the phased path's
+    one-shot grids for payloads of at least phased_min bytes (-1: off); else the persistent kernel."""
+    if world == 2 and 0 <= B <= oneshot_p2:
+        return "rs_phase_kernel<float,SUM,2> whole-array fold on both members between 2 one-workgroup team barriers"
     if phased_min >= 0 and B >= phased_min:
         return "rs_phase_kernel<float,SUM,P> + ag_phase_kernel between 3 one-workgroup team barriers"
     return "allreduce_kernel<float,SUM,vec>"
@@ -141,7 +144,8 @@ def roofline(world: int, share: int, B: int, kern_ms: float, kernel: str = "allr
                 "kernel": "fanin_kernel<uint8,OR,vec> (1-PE reduce = copy, 2B per launch)"}
         t_roof = 2 * B / (HBM_PEAK_GBS * 1e9)
     elif share > 1:
-        dev_bytes = share * (3.0 - 1.0 / world) * B
+        hbm_f = 3.0 if "whole-array" in kernel else 3.0 - 1.0 / world  # per PE: reads, then the dest write
+        dev_bytes = share * hbm_f * B
         roof = {"bound": "hbm", "achieved": dev_bytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "pes_per_device": share,
                 "traffic": pmc_traffic(f"{'phased' if kernel.startswith('rs_phase') else 'allreduce'}_{world}pe_same_device", B)
@@ -149,7 +153,7 @@ def roofline(world: int, share: int, B: int, kern_ms: float, kernel: str = "allr
                 "traffic_note": "device-wide FETCH_SIZE (x2) + WRITE_SIZE per launch, all PEs on one GPU "
                                 "(profiles/pmc_summary.json)",
                 "kernel": f"{kernel} x {share} co-located PEs "
-                          f"(device HBM traffic {share} x (3 - 1/p) x B per launch)"}
+                          f"(device HBM traffic {share} x {hbm_f:.3g} x B per launch)"}
         t_roof = dev_bytes / (HBM_PEAK_GBS * 1e9)
     else:
         link_bytes = 2.0 * (world - 1) / world * B  # RS + AG ingress per PE over p-1 links
@@ -158,7 +162,8 @@ def roofline(world: int, share: int, B: int, kern_ms: float, kernel: str = "allr
                 "traffic_note": "no PMC pass of a one-PE-per-GPU run is committed (the round's GPU "
                                 "pool has one GPU per box): HBM traffic per launch unmeasured",
                 "kernel": f"{kernel} (per-PE xGMI ingress 2(p-1)/p*B)"}
-        t_roof = max((3.0 - 1.0 / world) * B / (HBM_PEAK_GBS * 1e9),
+        hbm_f = 3.0 if "whole-array" in kernel else 3.0 - 1.0 / world
+        t_roof = max(hbm_f * B / (HBM_PEAK_GBS * 1e9),
                      (2.0 * B / world) / (XGMI_LINK_GBS * 1e9))
     frac = roof["achieved"] / roof["peak"]
     if frac > 1.0:
@@ -843,7 +848,8 @@ def main() -> int:
 
     share = int(ish.get_param("device_share")) if world > 1 else 1
     roof, t_roof = roofline(world, share, B, kern_ms,
-                            multi_pe_kernel(B, ish.get_param("phased_min_bytes")) if world > 1 else "")
+                            multi_pe_kernel(B, ish.get_param("phased_min_bytes"), world,
+                                            ish.get_param("oneshot_p2_max_bytes")) if world > 1 else "")
     algbw_roof = B / GiB / t_roof
     targets = {"algbw_roofline_GiBps": algbw_roof, "algbw_frac_of_roofline": algbw / algbw_roof}
     if algbw > algbw_roof:

@@ -246,6 +246,9 @@ struct PhaseArgs {
     // the payload bytes that bound the realigned loads; 0 = same phase.
     uint32_t shift;
     uint64_t total;
+    // 1: every member folds the WHOLE array (two-member direct path, runtime.cpp reduce_heap): the
+    // reduce-scatter grid over all items and both edges, no all-gather.
+    int whole;
 };
 hipError_t launch_rs_phase(int op, int dt, const PhaseArgs &a, hipStream_t s);
 hipError_t launch_ag_phase(const PhaseArgs &a, hipStream_t s);

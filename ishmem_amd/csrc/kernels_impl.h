@@ -1185,7 +1185,7 @@ __device__ __forceinline__ void rs_phase_edges(const PhaseArgs &a)
         const int tid = threadIdx.x;
         const uint64_t tail_off = a.head + a.nitems * (16 / sizeof(T));
         for (int region = 0; region < 2; ++region) {
-            const bool owner = region == 0 ? me == 0 : me == p - 1;
+            const bool owner = a.whole || (region == 0 ? me == 0 : me == p - 1);
             const uint64_t cnt = region == 0 ? a.head : a.tail;
             if (!owner || (uint64_t) tid >= cnt) continue;
             const uint64_t rbase = (region == 0 ? 0 : tail_off) * sizeof(T);
@@ -1206,8 +1206,8 @@ template <typename T, int OP, int P>
 __global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
 {
     const int me = a.me;
-    const uint64_t cs = min((uint64_t) me * a.items_per_chunk, a.nitems);
-    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
+    const uint64_t cs = a.whole ? 0 : min((uint64_t) me * a.items_per_chunk, a.nitems);
+    const uint64_t ce = a.whole ? a.nitems : min(cs + a.items_per_chunk, a.nitems);
     const uint64_t head_bytes = a.head * sizeof(T);
     const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
     auto body = [&](auto nt) {
@@ -1273,8 +1273,8 @@ __global__ __launch_bounds__(kRsRealignBlock) void rs_phase_realign_kernel(Phase
 {
     constexpr int BS = kRsRealignBlock, G = 4;
     __shared__ u32x4 edge[G][BS / 64 + 1];
-    const uint64_t cs = min((uint64_t) a.me * a.items_per_chunk, a.nitems);
-    const uint64_t ce = min(cs + a.items_per_chunk, a.nitems);
+    const uint64_t cs = a.whole ? 0 : min((uint64_t) a.me * a.items_per_chunk, a.nitems);
+    const uint64_t ce = a.whole ? a.nitems : min(cs + a.items_per_chunk, a.nitems);
     const uint64_t stride = (uint64_t) gridDim.x * BS;
     const uint64_t first = cs + (uint64_t) blockIdx.x * BS;
     if (cs + stride >= ce) {
@@ -1335,8 +1335,8 @@ int phase_grid(K, uint64_t items)
 template <typename T, int OP>
 hipError_t rs_phase_t(const PhaseArgs &a, hipStream_t s)
 {
-    const uint64_t cs = std::min((uint64_t) a.me * a.items_per_chunk, a.nitems);
-    const uint64_t len = std::min(cs + a.items_per_chunk, a.nitems) - cs;
+    const uint64_t cs = a.whole ? 0 : std::min((uint64_t) a.me * a.items_per_chunk, a.nitems);
+    const uint64_t len = a.whole ? a.nitems : std::min(cs + a.items_per_chunk, a.nitems) - cs;
     auto go = [&](auto kernel) {
         hipLaunchKernelGGL(kernel, dim3(phase_grid(kernel, len)), dim3(kFaninBlock), 0, s, a);
     };

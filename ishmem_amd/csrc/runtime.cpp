@@ -289,9 +289,10 @@ struct State {
     bool last_stream_set = false;
     bool stream_order = false;
     // Two-member teams fold the whole array in one phase up to this many bytes
-    // (ISHMEM_ONESHOT_P2_MAX_BYTES; above it the barrier saved is noise and RS + AG's lower HBM
-    // traffic wins where HBM, not the link, bounds).
-    long long oneshot_p2 = 64ll << 20;
+    // (ISHMEM_ONESHOT_P2_MAX_BYTES; round 5: barrier + fold grid + barrier, 1-16 MiB 9.5-22.6 us
+    // against 11.4-29 us; tied at 32 MiB on one GPU, where RS + AG's 2.5B of HBM per PE against
+    // 3B then wins — over one xGMI link both move B per direction).
+    long long oneshot_p2 = 32ll << 20;
     // Payloads of at least this many bytes (16-B vector body) take the phased reduce-scatter /
     // all-gather (two one-shot grids between one-workgroup barriers, kernels_impl.h) instead of
     // the persistent kernel (ISHMEM_PHASED_MIN_BYTES; kPhasedOff disables it).
@@ -314,6 +315,10 @@ struct State {
     // default 1): vector items laid out by dest, the sources read with unaligned 16-B loads;
     // 0 = the element-granular instantiation (A/B only).
     int ar_shifted = 1;
+    // Two-member disjoint reduces up to oneshot_p2 bytes: barrier + one whole-array fold grid +
+    // barrier (1, default) or the persistent kernel's one-shot mode (0; set_param "direct_p2",
+    // alike on every PE).
+    int direct_p2 = 1;
     // Team barriers of the phased paths and ishmem_team_sync: 0 = the one-workgroup barrier
     // kernel (team_sync_kernel), 1 = stream memory operations (ISHMEM_BARRIER_KIND=stream: the
     // command processor waits, no workgroup is held; team_barrier).  Agreed at init; sb_epoch is
@@ -775,10 +780,17 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         a.tail = pl.tail;
         a.items_per_chunk = pl.items_per_chunk;
         a.seg_items = pl.seg_items;
-    } else if ((pl.vec || realign) && (long long) nb >= s.phased_min) {
+    }
+    const bool disjoint = d0 + nb <= s0 || s0 + nb <= d0;
+    // Two members, disjoint buffers, up to oneshot_p2 bytes, 16-B body (or shifted sources):
+    // barrier, ONE one-shot grid in which each member folds the whole array from both sources,
+    // barrier (round 5, PhaseArgs::whole) — the phased path's shape without the all-gather and its
+    // barrier.  Over one link it moves the same B per direction as reduce-scatter + all-gather.
+    const bool direct = t.size == 2 && disjoint && (pl.vec || realign) && s.direct_p2 &&
+                        (long long) nb <= s.oneshot_p2;
+    if ((pl.vec || realign) && (direct || (long long) nb >= s.phased_min)) {
         // From phased_min bytes: barrier, one-shot reduce-scatter, barrier, one-shot all-gather,
         // barrier (kernels_impl.h, "Phased reduce-scatter + all-gather").  The barriers carry *ret.
-        // Checked before the two-member one-shot fold, which it beats from 32 MiB.
         PhaseArgs ph;
         memset(&ph, 0, sizeof(ph));
         for (int j = 0; j < t.size; ++j) {
@@ -794,6 +806,7 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         ph.p = t.size;
         ph.me = t.my_idx;
         ph.peer_nt = s.phased_peer_nt;
+        ph.whole = direct ? 1 : 0;
         if (realign) {
             const uint64_t h = std::min<uint64_t>(n, ((16 - d0 % 16) % 16) / es);
             ph.head = h;
@@ -813,16 +826,20 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         if (mark(1)) return 1;
         HIP_TRY(launch_rs_phase(op, dt, ph, st));
         if (mark(2)) return 1;
-        if (team_barrier(s, team, a, st)) return 1;
-        if (mark(3)) return 1;
-        HIP_TRY(launch_ag_phase(ph, st));
+        if (!direct) {
+            if (team_barrier(s, team, a, st)) return 1;
+            if (mark(3)) return 1;
+            HIP_TRY(launch_ag_phase(ph, st));
+        } else if (mark(3)) {
+            return 1;
+        }
         if (mark(4)) return 1;
         if (team_barrier(s, team, a, st)) return 1;
         if (mark(5)) return 1;
         s.phase_recorded = s.phase_recorded || ev;
         return 0;
     }
-    if (t.size == 2 && (long long) nb <= s.oneshot_p2 && (d0 + nb <= s0 || s0 + nb <= d0)) {
+    if (t.size == 2 && (long long) nb <= s.oneshot_p2 && disjoint) {
         a.oneshot = 1;
         a.items_per_chunk = pl.nitems;
         a.seg_items = seg_items(pl.nitems);
@@ -1532,7 +1549,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.debug = debug_level();
     s.trace = nullptr;
     s.stream_order = env_ll("ISHMEM_STREAM_ORDER", 0) != 0;
-    s.oneshot_p2 = std::max<long long>(0, env_bytes("ISHMEM_ONESHOT_P2_MAX_BYTES", 64ll << 20));
+    s.oneshot_p2 = std::max<long long>(0, env_bytes("ISHMEM_ONESHOT_P2_MAX_BYTES", 32ll << 20));
     s.phased_min = env_bytes("ISHMEM_PHASED_MIN_BYTES", kPhasedDefault);
     if (s.phased_min < 0) s.phased_min = kPhasedOff;
     s.staging_bytes = (env_size("ISHMEM_STAGING_SIZE", (size_t) 128 << 20) + kHeapAlign - 1) &
@@ -2754,6 +2771,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "realign_grid_cap") set_realign_grid_cap((int) std::min<long long>(std::max<long long>(value, 0), 1 << 30));
     else if (n == "collect_realign") set_collect_realign((int) (value != 0));
     else if (n == "ar_shifted") s.ar_shifted = value != 0;  // measurement: set alike on every PE
+    else if (n == "direct_p2") s.direct_p2 = value != 0;  // measurement: set alike on every PE
     else if (n == "phase_unaligned") set_phase_unaligned((int) (value != 0));
     else if (n == "stream_barrier_release") {
         // Escape hatch of the stream barrier, which has no timeout (team_barrier): store the team's
@@ -2800,6 +2818,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "realign_grid_cap") return realign_grid_cap();
     if (n == "collect_realign") return collect_realign();
     if (n == "ar_shifted") return s.ar_shifted;
+    if (n == "direct_p2") return s.direct_p2;
     if (n == "phase_unaligned") return phase_unaligned();
     if (n == "flags_fine_grained") return s.flags_kind != kFlagsCoarse ? 1 : 0;
     if (n == "flags_kind") return s.flags_kind;

@@ -89,6 +89,11 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             if int(ish.get_param("flags_kind")) != want:
                 fails.append(f"pe{pe} flags_kind {ish.get_param('flags_kind')} != agreed {want}")
 
+        if "nodirect" in scenarios:
+            # Two-member disjoint reduces on the persistent kernel's one-shot mode instead of the
+            # barrier-bracketed whole-array fold grid (set_param "direct_p2", alike on every PE).
+            ish.set_param("direct_p2", 0)
+
         if "realigncap" in scenarios:
             # Tests only: at most 3 workgroups for the realigned kernels, so the realigned
             # reduce-scatter's grid-stride loop (edge[] reuse between passes) runs at test sizes.

@@ -72,5 +72,10 @@ def test_multi_pe_kernel_follows_the_phased_threshold():
     assert k.startswith("rs_phase_kernel")
     assert b.multi_pe_kernel(B, -1).startswith("allreduce_kernel")
     assert b.multi_pe_kernel(64 << 20, 128 << 20).startswith("allreduce_kernel")
+    # Two members up to oneshot_p2: the whole-array fold between two barriers (HBM 3B per PE).
+    k2 = b.multi_pe_kernel(16 << 20, 4 << 20, 2, 32 << 20)
+    assert "whole-array" in k2 and b.multi_pe_kernel(64 << 20, 4 << 20, 2, 32 << 20).startswith("rs_phase_kernel<float,SUM,P>")
+    r2, t2 = b.roofline(2, 2, 16 << 20, 0.02, k2)
+    assert "2 x 3 x B" in r2["kernel"] and abs(t2 - 2 * 3 * (16 << 20) / 8e12) < 1e-12
     roof, _ = b.roofline(2, 2, B, 0.84, k)
     assert roof["kernel"].startswith("rs_phase_kernel") and 0 < roof["frac"] <= 1

@@ -169,6 +169,16 @@ def test_eight_pes_collect_scan_team():
             timeout=400)
 
 
+@pytest.mark.parametrize("direct", ["on", "off"])
+def test_two_pe_whole_array_fold(direct):
+    # Two members, disjoint buffers, no granule path, phased threshold off: every reduce up to
+    # oneshot_p2 bytes folds the whole array on both members — on (default) barrier + one fold
+    # grid + barrier (PhaseArgs::whole), off the persistent kernel's one-shot mode.  Golden inputs,
+    # offset sweeps (shifted sources), edges, hipGraph replay, the tripwire.
+    scen = ["golden", "offsets", "offsets_large", "edge", "graph", "tripwire"] + (["nodirect"] if direct == "off" else [])
+    run_pes(2, scen, env={"ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_PHASED_MIN_BYTES": -1, "ISHMEM_MAX_BLOCKS": 64})
+
+
 def test_two_pe_reduce_scatter_allgather_path():
     # At 2 PEs non-in-place reduces take the one-shot fold (below 16 MiB) or the phased path by
     # default; force the persistent RS + AG kernel (and no LL) for the same golden / offset /
