@@ -272,7 +272,8 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
  * device-side spin), "stream_order" (1: collectives issued on different streams are ordered by
  * the library in call order, ~2 us per call; 0, the default: the caller orders them, as the
  * reference requires), "oneshot_p2_max_bytes" (two-member teams: one-phase fold up to this size,
- * default 64 MiB), "phased_min_bytes" (payloads of at least this size take the phased path:
+ * default 32 MiB), "direct_p2" (1, default: that fold as barrier + one grid + barrier; 0: the
+ * persistent kernel's one-shot mode), "phased_min_bytes" (payloads of at least this size take the phased path:
  * barrier, one-shot reduce-scatter, barrier, one-shot all-gather, barrier; -1 disables it),
  * "phase_events" (1: the next phased reduces record HIP events between their five launches, read
  * with ishmemi_c_phase_times; a measurement hook), "debug"; A/B switches for measurements, set

@@ -1291,10 +1291,12 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
         const uint64_t seg = ipc_max * (uint64_t) t.size;
         if (ipc_max == 0) return fail("scan: staging region too small for this team");
         const uintptr_t d0 = (uintptr_t) dst, s0 = (uintptr_t) src, nb = n * es;
-        if (t.size == 2 && (long long) nb >= s.phased_min && (d0 + nb <= s0 || s0 + nb <= d0)) {
+        if (t.size == 2 && (d0 + nb <= s0 || s0 + nb <= d0)) {
             // Two members, disjoint buffers: barrier, direct one-shot fold, barrier (no scratch;
             // kernels_coll.hip scan_direct_kernel).  Every member sees the same n and the same
-            // symmetric offsets, so all take this path together.
+            // symmetric offsets, so all take this path together.  At every size past the granule
+            // path since round 5 (it was the phased threshold's): 1 / 2 MiB 8.9-9.3 / 9.0 us
+            // against the scratch kernel's 17.8-18.1 / 19.7-20.8 (profiles/r05/scan/).
             if (order_stream(s, st)) return 1;
             ScanArgs a;
             memset(&a, 0, sizeof(a));
