@@ -319,6 +319,7 @@ struct State {
     // barrier (1, default) or the persistent kernel's one-shot mode (0; set_param "direct_p2",
     // alike on every PE).
     int direct_p2 = 1;
+    int direct_max_pes = 2;  // measurement (set_param "direct_max_pes"): the whole-array fold for larger teams too
     // Team barriers of the phased paths and ishmem_team_sync: 0 = the one-workgroup barrier
     // kernel (team_sync_kernel), 1 = stream memory operations (ISHMEM_BARRIER_KIND=stream: the
     // command processor waits, no workgroup is held; team_barrier).  Agreed at init; sb_epoch is
@@ -786,8 +787,8 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     // barrier, ONE one-shot grid in which each member folds the whole array from both sources,
     // barrier (round 5, PhaseArgs::whole) — the phased path's shape without the all-gather and its
     // barrier.  Over one link it moves the same B per direction as reduce-scatter + all-gather.
-    const bool direct = t.size == 2 && disjoint && (pl.vec || realign) && s.direct_p2 &&
-                        (long long) nb <= s.oneshot_p2;
+    const bool direct = (t.size == 2 || t.size <= s.direct_max_pes) && disjoint && (pl.vec || realign) &&
+                        s.direct_p2 && (long long) nb <= s.oneshot_p2;
     if ((pl.vec || realign) && (direct || (long long) nb >= s.phased_min)) {
         // From phased_min bytes: barrier, one-shot reduce-scatter, barrier, one-shot all-gather,
         // barrier (kernels_impl.h, "Phased reduce-scatter + all-gather").  The barriers carry *ret.
@@ -2774,6 +2775,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "collect_realign") set_collect_realign((int) (value != 0));
     else if (n == "ar_shifted") s.ar_shifted = value != 0;  // measurement: set alike on every PE
     else if (n == "direct_p2") s.direct_p2 = value != 0;  // measurement: set alike on every PE
+    else if (n == "direct_max_pes") s.direct_max_pes = (int) std::min<long long>(std::max<long long>(value, 2), kMaxPes);
     else if (n == "phase_unaligned") set_phase_unaligned((int) (value != 0));
     else if (n == "stream_barrier_release") {
         // Escape hatch of the stream barrier, which has no timeout (team_barrier): store the team's
@@ -2821,6 +2823,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "collect_realign") return collect_realign();
     if (n == "ar_shifted") return s.ar_shifted;
     if (n == "direct_p2") return s.direct_p2;
+    if (n == "direct_max_pes") return s.direct_max_pes;
     if (n == "phase_unaligned") return phase_unaligned();
     if (n == "flags_fine_grained") return s.flags_kind != kFlagsCoarse ? 1 : 0;
     if (n == "flags_kind") return s.flags_kind;
