@@ -119,8 +119,9 @@ def multi_pe_kernel(B: int, phased_min: int, world: int = 0, oneshot_p2: int = -
     """The multi-PE kernels a B-byte f32 sum with disjoint buffers takes (runtime.cpp reduce_heap):
     two members up to oneshot_p2 bytes fold the whole array between two barriers; the phased path's
     one-shot grids for payloads of at least phased_min bytes (-1: off); else the persistent kernel."""
-    if world == 2 and 0 <= B <= oneshot_p2:
-        return "rs_phase_kernel<float,SUM,2> whole-array fold on both members between 2 one-workgroup team barriers"
+    if (world == 2 and 0 <= B <= oneshot_p2) or (3 <= world <= 4 and 0 <= (world - 1) * B <= oneshot_p2 // 4):
+        return (f"rs_phase_kernel<float,SUM,{world}> whole-array fold on every member between 2 one-workgroup "
+                "team barriers")
     if phased_min >= 0 and B >= phased_min:
         return "rs_phase_kernel<float,SUM,P> + ag_phase_kernel between 3 one-workgroup team barriers"
     return "allreduce_kernel<float,SUM,vec>"
@@ -144,7 +145,7 @@ def roofline(world: int, share: int, B: int, kern_ms: float, kernel: str = "allr
                 "kernel": "fanin_kernel<uint8,OR,vec> (1-PE reduce = copy, 2B per launch)"}
         t_roof = 2 * B / (HBM_PEAK_GBS * 1e9)
     elif share > 1:
-        hbm_f = 3.0 if "whole-array" in kernel else 3.0 - 1.0 / world  # per PE: reads, then the dest write
+        hbm_f = world + 1.0 if "whole-array" in kernel else 3.0 - 1.0 / world  # per PE: reads, then the dest write
         dev_bytes = share * hbm_f * B
         roof = {"bound": "hbm", "achieved": dev_bytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "pes_per_device": share,
@@ -156,15 +157,16 @@ def roofline(world: int, share: int, B: int, kern_ms: float, kernel: str = "allr
                           f"(device HBM traffic {share} x {hbm_f:.3g} x B per launch)"}
         t_roof = dev_bytes / (HBM_PEAK_GBS * 1e9)
     else:
-        link_bytes = 2.0 * (world - 1) / world * B  # RS + AG ingress per PE over p-1 links
+        whole = "whole-array" in kernel  # each member pulls every peer's whole source
+        link_bytes = (world - 1.0) * B if whole else 2.0 * (world - 1) / world * B  # ingress per PE, p-1 links
         roof = {"bound": "xgmi", "achieved": link_bytes / t / 1e9,
                 "peak": XGMI_LINK_GBS * (world - 1), "unit": "GB/s", "traffic": None,
                 "traffic_note": "no PMC pass of a one-PE-per-GPU run is committed (the round's GPU "
                                 "pool has one GPU per box): HBM traffic per launch unmeasured",
-                "kernel": f"{kernel} (per-PE xGMI ingress 2(p-1)/p*B)"}
-        hbm_f = 3.0 if "whole-array" in kernel else 3.0 - 1.0 / world
+                "kernel": f"{kernel} (per-PE xGMI ingress {'(p-1)*B' if whole else '2(p-1)/p*B'})"}
+        hbm_f = world + 1.0 if whole else 3.0 - 1.0 / world
         t_roof = max(hbm_f * B / (HBM_PEAK_GBS * 1e9),
-                     (2.0 * B / world) / (XGMI_LINK_GBS * 1e9))
+                     (link_bytes / (world - 1)) / (XGMI_LINK_GBS * 1e9))
     frac = roof["achieved"] / roof["peak"]
     if frac > 1.0:
         roof.update(frac=None, frac_raw=frac, model_violated=True,
@@ -237,6 +239,7 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max, share: int = 
     min / max winner rotating over the PEs)."""
     from ishmem_amd import selfcheck as sc
     out = []
+    phased_min, oneshot_p2 = ish.get_param("phased_min_bytes"), ish.get_param("oneshot_p2_max_bytes")
     for dtn, npd in (("int32", np.int32), ("double", np.float64)):
         es = np.dtype(npd).itemsize
         nmax = nbytes_max // es
@@ -277,7 +280,8 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max, share: int = 
                     wins += [(int(x), 4096) for x in np.random.default_rng(5).integers(0, n - 4096, 8)]
                 bad = sum(sc.count_wrong(hip, dst, op, npd, world, lo, m) for lo, m in wins)
                 bad = int(max_over_ranks(dist, [float(bad)])[0])
-                _, t_roof = roofline(world, share, nb, us * 1e-3)
+                _, t_roof = roofline(world, share, nb, us * 1e-3,
+                                     multi_pe_kernel(nb, phased_min, world, oneshot_p2))
                 out.append({"op": op, "dtype": dtn, "bytes": nb, "us": round(us, 2),
                             "algbw_GiBps": round(nb / GiB / (us * 1e-6), 2),
                             # t_roof / t: the same bound as the line's roofline (xGMI links one PE

@@ -319,7 +319,7 @@ struct State {
     // barrier (1, default) or the persistent kernel's one-shot mode (0; set_param "direct_p2",
     // alike on every PE).
     int direct_p2 = 1;
-    int direct_max_pes = 2;  // measurement (set_param "direct_max_pes"): the whole-array fold for larger teams too
+    int direct_max_pes = 4;  // the whole-array fold up to this team size (set_param "direct_max_pes", >= 2)
     // Team barriers of the phased paths and ishmem_team_sync: 0 = the one-workgroup barrier
     // kernel (team_sync_kernel), 1 = stream memory operations (ISHMEM_BARRIER_KIND=stream: the
     // command processor waits, no workgroup is held; team_barrier).  Agreed at init; sb_epoch is
@@ -787,8 +787,14 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     // barrier, ONE one-shot grid in which each member folds the whole array from both sources,
     // barrier (round 5, PhaseArgs::whole) — the phased path's shape without the all-gather and its
     // barrier.  Over one link it moves the same B per direction as reduce-scatter + all-gather.
-    const bool direct = (t.size == 2 || t.size <= s.direct_max_pes) && disjoint && (pl.vec || realign) &&
-                        s.direct_p2 && (long long) nb <= s.oneshot_p2;
+    // Three or four members (round 5): the same whole-array fold while (p - 1) * B <= oneshot_p2 / 4
+    // (8 MiB of peer reads per member by default: 4 MiB at 3 PEs, 2.67 MiB at 4).  On one GPU it
+    // beat the persistent / phased paths up to 8 MiB at 3 PEs and 4 MiB at 4 (1 / 2 MiB at 4 PEs:
+    // 11.3-12.5 / 11.5-12.6 us against 17.9-18.5 / 25.3-25.4); each member pulls (p - 1) * B over
+    // the links where reduce-scatter + all-gather pulls 2(p - 1) / p * B, hence the tighter bound.
+    const bool direct = disjoint && (pl.vec || realign) && s.direct_p2 && t.size <= s.direct_max_pes &&
+                        (t.size == 2 ? (long long) nb <= s.oneshot_p2
+                                     : (long long) ((uint64_t) (t.size - 1) * nb) <= s.oneshot_p2 / 4);
     if ((pl.vec || realign) && (direct || (long long) nb >= s.phased_min)) {
         // From phased_min bytes: barrier, one-shot reduce-scatter, barrier, one-shot all-gather,
         // barrier (kernels_impl.h, "Phased reduce-scatter + all-gather").  The barriers carry *ret.

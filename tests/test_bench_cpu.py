@@ -77,5 +77,10 @@ def test_multi_pe_kernel_follows_the_phased_threshold():
     assert "whole-array" in k2 and b.multi_pe_kernel(64 << 20, 4 << 20, 2, 32 << 20).startswith("rs_phase_kernel<float,SUM,P>")
     r2, t2 = b.roofline(2, 2, 16 << 20, 0.02, k2)
     assert "2 x 3 x B" in r2["kernel"] and abs(t2 - 2 * 3 * (16 << 20) / 8e12) < 1e-12
+    # Three / four members while (p - 1) * B <= oneshot_p2 / 4; every member pulls (p - 1) * B.
+    k4 = b.multi_pe_kernel(2 << 20, 4 << 20, 4, 32 << 20)
+    assert "whole-array" in k4 and "whole-array" not in b.multi_pe_kernel(4 << 20, 4 << 20, 4, 32 << 20)
+    r4, t4 = b.roofline(4, 1, 2 << 20, 0.02, k4)
+    assert "(p-1)*B" in r4["kernel"] and abs(t4 - max(5 * (2 << 20) / 8e12, (2 << 20) / 153.6e9)) < 1e-12
     roof, _ = b.roofline(2, 2, B, 0.84, k)
     assert roof["kernel"].startswith("rs_phase_kernel") and 0 < roof["frac"] <= 1
