@@ -1298,12 +1298,15 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
         const uint64_t seg = ipc_max * (uint64_t) t.size;
         if (ipc_max == 0) return fail("scan: staging region too small for this team");
         const uintptr_t d0 = (uintptr_t) dst, s0 = (uintptr_t) src, nb = n * es;
-        if (t.size == 2 && (d0 + nb <= s0 || s0 + nb <= d0)) {
+        const bool disjoint = d0 + nb <= s0 || s0 + nb <= d0;
+        if (disjoint && (t.size == 2 || (t.size <= s.direct_max_pes &&
+                                         (long long) ((uint64_t) (t.size - 1) * nb) <= s.oneshot_p2 / 4))) {
             // Two members, disjoint buffers: barrier, direct one-shot fold, barrier (no scratch;
             // kernels_coll.hip scan_direct_kernel).  Every member sees the same n and the same
             // symmetric offsets, so all take this path together.  At every size past the granule
             // path since round 5 (it was the phased threshold's): 1 / 2 MiB 8.9-9.3 / 9.0 us
-            // against the scratch kernel's 17.8-18.1 / 19.7-20.8 (profiles/r05/scan/).
+            // against the scratch kernel's 17.8-18.1 / 19.7-20.8 (profiles/r05/scan/).  Three and
+            // four members under the reduce's whole-array bound ((p - 1) * B <= oneshot_p2 / 4).
             if (order_stream(s, st)) return 1;
             ScanArgs a;
             memset(&a, 0, sizeof(a));
