@@ -395,7 +395,8 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     if world == 2:
         run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
         run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)
-    cap = int(ish.get_param("ll_capacity_bytes"))  # the ring's capacity at this team size
+    cap = int(ish.get_param("ll_capacity_bytes"))  # the ring's capacity at this team size (the leg
+    # times the granule path up to it, past the default threshold ll_limit_bytes where that is lower)
     for nb in (4096, 16384, 65536, 131072, 262144, 524288):
         if nb <= cap:
             run("ll_on", "ll_max_bytes", cap, nb, 50)

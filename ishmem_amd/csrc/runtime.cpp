@@ -610,11 +610,22 @@ int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)
 // ll_load / ll_store): one-hop push of {data, epoch} granules into the peers' rings, no barriers
 // (ll_kernel).  The choice depends on the byte count and the team size only, which every member
 // shares.
+// Teams that take the whole-array fold (3 or 4 members, reduce_heap "direct") leave it the sizes
+// from 768 KiB / p: the fold costs a flat ~9-10 us at 256 KiB - 2 MiB on one GPU where the granule
+// path grows with p (4 PEs: 11.0-11.6 us at 256 KiB, 15.1-15.6 at 512 KiB; 3 PEs: 9.0-9.3 / 12.1;
+// profiles/r05/direct_p2/r05zzd_ab.txt).
+size_t ll_limit(const State &s, int p)
+{
+    size_t lim = std::min<size_t>((size_t) std::max<long long>(s.ll_max_bytes, 0), ll_capacity(p));
+    if (p >= 3 && p <= s.direct_max_pes && s.direct_p2) lim = std::min<size_t>(lim, (768u << 10) / (size_t) p);
+    return lim;
+}
+
 bool ll_eligible(const State &s, const Team &t, const void *dst, const void *src, size_t bytes)
 {
     (void) dst;
     (void) src;
-    return t.size > 1 && bytes > 0 && (long long) bytes <= s.ll_max_bytes && bytes <= ll_capacity(t.size);
+    return t.size > 1 && bytes > 0 && bytes <= ll_limit(s, t.size);
 }
 
 // Collectives of one PE run in the order they were called, whatever streams they were enqueued
@@ -2825,6 +2836,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "phased_min_bytes") return s.phased_min == kPhasedOff ? -1 : s.phased_min;
     if (n == "ll_max_bytes") return s.ll_max_bytes;
     if (n == "ll_capacity_bytes") return (long long) ll_capacity(s.npes);  // TEAM_WORLD's ring capacity
+    if (n == "ll_limit_bytes") return (long long) ll_limit(s, s.npes);     // TEAM_WORLD's granule threshold
     if (n == "debug") return s.debug;
     if (n == "phased_peer_nt") return s.phased_peer_nt;
     if (n == "barrier_kind") return s.barrier_kind;

@@ -1002,7 +1002,7 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             # so the device-side skew varies; every dest then checked against the oracle.
             import time as _t
             rng = np.random.default_rng(4242)
-            cap = min(int(ish.get_param("ll_max_bytes")), int(ish.get_param("ll_capacity_bytes")))
+            cap = int(ish.get_param("ll_limit_bytes"))  # the granule path's threshold for this team size
             K = 32
             plan = []
             for k in range(K):
@@ -1142,7 +1142,7 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                         break
                 hip.stream_synchronize(occ)
                 done_iters += 1
-                ll_cap = min(int(ish.get_param("ll_max_bytes")), (1 << 20) // len(members))  # kernels.h ll_capacity
+                ll_cap = min(int(ish.get_param("ll_max_bytes")), (2 << 20) // len(members))  # about kernels.h ll_capacity
                 kinds.add("ll" if n * es <= ll_cap else ("big" if n * es > (1 << 20) else "mid"))
                 occupied += occupier >= 0
             if pe == 0:
