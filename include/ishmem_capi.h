@@ -286,7 +286,8 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
  * agrees on them (the minimum over the PEs; the maximum for "phased_min_bytes") and a later
  * set_param must be made with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,
  * nothing is paired by workgroup index).  ishmemi_c_get_param also reports "staging_bytes",
- * "heap_bytes", "flags_fine_grained", "cu_count" (compute units of this PE's device) and
+ * "heap_bytes", "flags_fine_grained", "ll_capacity_bytes" / "ll_limit_bytes" (TEAM_WORLD's granule
+ * ring capacity / threshold), "cu_count" (compute units of this PE's device) and
  * "device_share" (PEs of the job on this PE's device: 1 with one PE per GPU). */
 const char *ishmemi_c_last_error(void);
 int ishmemi_c_set_param(const char *name, long long value);
