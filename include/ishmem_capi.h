@@ -281,7 +281,10 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
  * another 16-B phase than dest, read with unaligned loads; 0: element-granular), "phase_unaligned"
  * (1, default: the phased reduce-scatter reads such sources with unaligned 16-B loads; 0: the
  * realigning kernel), "collect_realign" (1, default: collect members off the 16-B grid realigned;
- * 0: narrow items), "barrier_kind" (0 kernel, 1 stream memory operations).  "ll_max_bytes",
+ * 0: narrow items), "barrier_kind" (0 kernel, 1 stream memory operations), "block_spin" (blocking
+ * calls' wait: 2, default, spin on a stream-written host word; 1 the spin then
+ * hipStreamSynchronize; 0 hipStreamSynchronize), "direct_max_pes" (largest team taking the
+ * whole-array fold, default 4).  "ll_max_bytes",
  * "oneshot_p2_max_bytes" and "phased_min_bytes" choose the kernels of a multi-PE call: init
  * agrees on them (the minimum over the PEs; the maximum for "phased_min_bytes") and a later
  * set_param must be made with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,

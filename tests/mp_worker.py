@@ -994,6 +994,45 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 ish.ishmem_free(b_)
             ish.set_param("max_blocks", int(os.environ.get("ISHMEM_MAX_BLOCKS", 1024)))
 
+        if "blockread" in scenarios:
+            # Blocking calls return once a stream write after their launches has reached host
+            # memory (runtime.cpp host_wait, block_spin 2, the default): dest must then be final
+            # for work on ANY stream — read here right away through a non-blocking stream (not
+            # ordered after the null stream), new inputs every round, granule / fold / phased
+            # sizes, reduce / fcollect / scan / broadcast.
+            nbst = hip.stream_create()
+            cases = [(n, kind) for n in (100, 70_001, 1_000_003) for kind in ("reduce", "fcollect", "inscan", "broadcast")]
+            nmax = 1_000_003
+            src_r = ish.ishmem_malloc(4 * nmax)
+            dst_r = ish.ishmem_malloc(4 * nmax * npes)
+            hbuf = hip.host_malloc(4 * nmax * npes)
+            hv = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_int32 * (nmax * npes)).from_address(hbuf))
+            for rnd in range(3):
+                for n, kind in cases:
+                    ins = [oracle.fill_random(DT["int32"], 7000 + 97 * rnd + 13 * j + n, n) for j in range(npes)]
+                    hip.upload(src_r, ins[pe])
+                    ish.ishmem_barrier_all()
+                    if kind == "reduce":
+                        r, want = ish.ishmem_int32_sum_reduce(dst_r, src_r, n), oracle.reduce_fold(OPS["sum"], DT["int32"], ins, 0)
+                    elif kind == "fcollect":
+                        r, want = ish.ishmem_int32_fcollect(dst_r, src_r, n), np.concatenate(ins)
+                    elif kind == "inscan":
+                        r, want = ish.scan("int32", True, dst_r, src_r, n), oracle.scan_fold(DT["int32"], ins, pe, True)
+                    else:
+                        root = rnd % npes
+                        r, want = ish.ishmem_int32_broadcast(dst_r, src_r, n, root), ins[root]
+                    if r:
+                        fails.append(f"pe{pe} blockread {kind} n={n}: rc={r} {ish.last_error()}")
+                        continue
+                    hip.memcpy_async(hbuf, dst_r, 4 * want.size, nbst)
+                    hip.stream_synchronize(nbst)
+                    if not np.array_equal(hv[:want.size], want.view(np.int32)):
+                        fails.append(f"pe{pe} blockread {kind} n={n} round {rnd}: dest not final when the call returned")
+            hip.stream_destroy(nbst)
+            hip.host_free(hbuf)
+            ish.ishmem_free(dst_r)
+            ish.ishmem_free(src_r)
+
         if "llchain" in scenarios:
             # Granule-path collectives back to back on one stream with no host synchronisation
             # (round 5: reduce, fcollect, inclusive / exclusive scan, broadcast share the rings, whose two

@@ -95,6 +95,13 @@ def test_huge_2p5GiB_per_pe_head_tail_and_2GiB_boundary():
     run_pes(2, ["huge"], env={"ISHMEM_MAX_BLOCKS": 64, "ISHMEM_SYMMETRIC_SIZE": "6G"}, timeout=400)
 
 
+@pytest.mark.parametrize("npes", [2, 3, 4])
+def test_blocking_calls_return_with_dest_final_for_any_stream(npes):
+    # The blocking calls' host wait (a stream-written completion word, no hipStreamSynchronize):
+    # dest read at once through a non-blocking stream, every kind of blocking collective.
+    run_pes(npes, ["blockread"], timeout=200)
+
+
 @pytest.mark.parametrize("npes", [2, 3, 4, 8])
 def test_granule_collectives_chained_without_sync(npes):
     # 32 granule-path reduces / fcollects / scans back to back on one stream, random sizes up to
