@@ -338,7 +338,9 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
                three team barriers as the one-workgroup barrier kernel (default) or as stream
                memory operations (ISHMEM_BARRIER_KIND=stream: the command processor waits);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
-      ll    - 4 KiB up to the granule ring's capacity (1 MiB / team size) with the one-hop granule
+      fold  - 512 KiB - 4 MiB: the whole-array fold between two barriers forced for this team
+              size against the path without it (granule path off in both);
+      ll    - 4 KiB up to the granule ring's capacity (2 MiB / team size) with the one-hop granule
               path on (default) and off."""
 
     def timed(n, iters):
@@ -395,6 +397,14 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     if world == 2:
         run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
         run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)
+    # The whole-array fold (two barriers around one grid in which every member folds every
+    # member's source) against the default path below it, at mid sizes: decided on one GPU for
+    # 2-4 PEs; over xGMI each member pulls (p - 1) * B instead of 2(p - 1)/p * B.
+    for nb in (512 << 10, 1 << 20, 2 << 20, 4 << 20):
+        if nb <= B:
+            run("fold", "direct_max_pes", max(2, world), nb, 20,
+                also={"direct_p2": 1, "oneshot_p2_max_bytes": 1 << 40, "ll_max_bytes": 0})
+            run("no_fold", "direct_p2", 0, nb, 20, also={"ll_max_bytes": 0})
     cap = int(ish.get_param("ll_capacity_bytes"))  # the ring's capacity at this team size (the leg
     # times the granule path up to it, past the default threshold ll_limit_bytes where that is lower)
     for nb in (4096, 16384, 65536, 131072, 262144, 524288):
