@@ -89,6 +89,12 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             if int(ish.get_param("flags_kind")) != want:
                 fails.append(f"pe{pe} flags_kind {ish.get_param('flags_kind')} != agreed {want}")
 
+        if "arshift0" in scenarios:
+            # The persistent kernel's element-granular instantiation for sources on another 16-B
+            # phase than dest (set_param "ar_shifted" 0; the default keeps 16-B items and reads
+            # the sources with unaligned loads).
+            ish.set_param("ar_shifted", 0)
+
         if "nodirect" in scenarios:
             # Two-member disjoint reduces on the persistent kernel's one-shot mode instead of the
             # barrier-bracketed whole-array fold grid (set_param "direct_p2", alike on every PE).

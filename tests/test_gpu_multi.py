@@ -186,6 +186,16 @@ def test_two_pe_whole_array_fold(direct):
     run_pes(2, scen, env={"ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_PHASED_MIN_BYTES": -1, "ISHMEM_MAX_BLOCKS": 64})
 
 
+@pytest.mark.parametrize("npes", [2, 3])
+@pytest.mark.parametrize("shifted", ["vector", "element"])
+def test_persistent_kernel_with_shifted_sources(npes, shifted):
+    # Sources on another 16-B phase than dest on the persistent kernel (no granule path, no
+    # whole-array fold, no phased path): 16-B items laid out by dest with unaligned source loads
+    # (default) or the element-granular instantiation (ar_shifted 0); guard bytes checked.
+    scen = ["offsets", "offsets_large", "nodirect"] + (["arshift0"] if shifted == "element" else [])
+    run_pes(npes, scen, env={"ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_PHASED_MIN_BYTES": -1, "ISHMEM_MAX_BLOCKS": 64})
+
+
 def test_two_pe_reduce_scatter_allgather_path():
     # At 2 PEs non-in-place reduces take the one-shot fold (below 16 MiB) or the phased path by
     # default; force the persistent RS + AG kernel (and no LL) for the same golden / offset /
