@@ -810,14 +810,13 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     a.tail = pl.tail;
     a.items_per_chunk = pl.items_per_chunk;
     a.seg_items = pl.seg_items;
-    // Two members: reduce-scatter + all-gather moves B over the one link in two halves with a
-    // hand-off between; a one-shot fold of the whole array moves the same B with no hand-off.
-    // Not in place (a member would overwrite its source while the peer still reads it).  The
-    // choice depends only on symmetric-address properties, so every member makes the same one.
+    // Every choice below depends only on symmetric-address properties, the byte count, the team
+    // size and parameters agreed at init, so every member makes the same one.
     const uintptr_t d0 = (uintptr_t) dst, s0 = (uintptr_t) src, nb = n * es;
     // Source and dest on different 16-B phases (same on every PE: the offsets are symmetric): the
-    // phased grids realign the sources (rs_phase_kernel, a.shift) instead of the persistent
-    // kernel's element-granular path.
+    // phased / whole-array grids keep dest's 16-B items and read the sources with unaligned loads
+    // (PhaseArgs::shift; phase_unaligned 0: the realigning kernel), the persistent kernel likewise
+    // below (ar_shifted), instead of an element-granular path.
     const bool realign = !pl.vec && d0 % es == 0 && s0 % es == 0 && nb >= kRealignMinBytes;
     if (realign && (long long) nb < s.phased_min && s.ar_shifted) {
         // Below phased_min: the persistent kernel's vector instantiation with items laid out by
