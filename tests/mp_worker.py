@@ -384,6 +384,18 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
                 else:
                     check(f"inplace {op} {dt} {n}", op, dt, ins, hip.download(b, n, oracle.NP[dt]))
                 ish.ishmem_free(b)
+            # Larger in place, dest 4 B off the 16-B grid (head / tail elements): the whole-array
+            # fold through the staging region at 2-4 PEs (round 5), the phased path above it.
+            for n in (786_435, 3_000_001):
+                ins = [oracle.fill_random(DT["float"], 91 + j, n) for j in range(npes)]
+                b = heap(n + 8, DT["float"])
+                hip.upload(b + 4, ins[pe])
+                r = ish.reduce("sum", "float", b + 4, b + 4, n)
+                if r:
+                    fails.append(f"pe{pe} inplace offset n={n} rc={r} {ish.last_error()}")
+                else:
+                    check(f"inplace offset sum float {n}", OPS["sum"], DT["float"], ins, hip.download(b + 4, n, np.float32))
+                ish.ishmem_free(b)
 
         if "offsets" in scenarios:
             # The reference tester's offset sweep (ishmem_tester.h:1407-1436): nelems 1..16 x

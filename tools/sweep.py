@@ -34,6 +34,8 @@ def main() -> None:
                     "HIP events between the phased path's five launches (rank 0's ms)")
     ap.add_argument("--emulate-share1", action="store_true",
                     help="every PE reports its own device (ISHMEM_TEST_PCI_BUS): the launch shapes of one PE per GPU")
+    ap.add_argument("--inplace", action="store_true",
+                    help="reduce: source == dest (the values then change every call: ok = -1, not checked)")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
                     help="ishmem set_param before the sweep (every PE alike), repeatable")
     args = ap.parse_args()
@@ -86,6 +88,8 @@ def main() -> None:
             return ish.broadcast_on_stream(dst, src, n * 4, 0, 0, st)
         if args.coll == "inscan":
             return ish.lib().ishmemi_c_scan_on_stream(0, ish.DTYPES["float"], 1, dst, src, n, None, st)
+        if args.inplace:
+            return ish.ishmemx_float_sum_reduce_on_stream(src + 4 * so, src + 4 * so, n, 0, st)
         return ish.ishmemx_float_sum_reduce_on_stream(dst + 4 * do, src + 4 * so, n, 0, st)
 
     def expect(i, n):
@@ -142,7 +146,7 @@ def main() -> None:
         k = min(n, 64)
         last = n * (world if args.coll == "fcollect" else 1)
         got = hip.download(dst + 4 * do + (last - k) * 4, k, np.float32)
-        ok = bool(np.array_equal(got, expect(np.arange(n - k, n), n)))
+        ok = -1 if args.inplace else int(np.array_equal(got, expect(np.arange(n - k, n), n)))
         if rank == 0:
             print(f"{n * 4},{us:.2f},{n * 4 / 2**30 / (us * 1e-6):.2f},{int(ok)}", flush=True)
         n *= args.factor
