@@ -328,7 +328,10 @@ struct State {
     // barrier (1, default) or the persistent kernel's one-shot mode (0; set_param "direct_p2",
     // alike on every PE).
     int direct_p2 = 1;
-    int direct_max_pes = 4;  // the whole-array fold up to this team size (set_param "direct_max_pes", >= 2)
+    int direct_max_pes = 4;
+    int direct_inplace = 1;
+    char *fold_scratch[kMaxTeams] = {};  // in-place whole-array fold: team-private device scratch
+    size_t fold_scratch_bytes[kMaxTeams] = {};  // the whole-array fold up to this team size (set_param "direct_max_pes", >= 2)
     // Team barriers of the phased paths and ishmem_team_sync: 0 = the one-workgroup barrier
     // kernel (team_sync_kernel), 1 = stream memory operations (ISHMEM_BARRIER_KIND=stream: the
     // command processor waits, no workgroup is held; team_barrier).  Agreed at init; sb_epoch is
@@ -842,9 +845,40 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
     // beat the persistent / phased paths up to 8 MiB at 3 PEs and 4 MiB at 4 (1 / 2 MiB at 4 PEs:
     // 11.3-12.5 / 11.5-12.6 us against 17.9-18.5 / 25.3-25.4); each member pulls (p - 1) * B over
     // the links where reduce-scatter + all-gather pulls 2(p - 1) / p * B, hence the tighter bound.
-    const bool direct = disjoint && (pl.vec || realign) && s.direct_p2 && t.size <= s.direct_max_pes &&
-                        (t.size == 2 ? (long long) nb <= s.oneshot_p2
-                                     : (long long) ((uint64_t) (t.size - 1) * nb) <= s.oneshot_p2 / 4);
+    const bool fold_size = s.direct_p2 && t.size <= s.direct_max_pes &&
+                           (t.size == 2 ? (long long) nb <= s.oneshot_p2
+                                        : (long long) ((uint64_t) (t.size - 1) * nb) <= s.oneshot_p2 / 4);
+    // In place (source == dest): the same fold into a team-private scratch buffer on this device
+    // (dest's 16-B phase; peers never read it, so it is plain device memory, grown on demand),
+    // the end barrier (every member has read every source), then a local copy into dest.  The
+    // staging region with its events was tried first and lost to the persistent kernel
+    // (profiles/r05/direct_p2/r05zzp_*); set_param "direct_inplace" 0 turns this off.
+    char *scratch = nullptr;
+    // Only while p * B <= 4 MiB: the copy back costs 2B of HBM and a launch, and the fold's gain
+    // over the persistent kernel is gone by 2 MiB at 2 PEs and 1 MiB at 4 (2 PEs 1 MiB 12.8-13.4
+    // vs 14.9-15.4 us, 4 MiB 20.6-22.4 vs 18.6-19.5; 4 PEs 512 KiB 14.2-14.7 vs 19.7-21.3;
+    // profiles/r05/direct_p2/r05zzs_ab_inplace_scratch.txt).
+    if (fold_size && d0 == s0 && pl.vec && s.direct_inplace && (uint64_t) t.size * nb <= (4u << 20) &&
+        !capturing(st)) {
+        const size_t need = nb + 16;
+        if (s.fold_scratch_bytes[team] < need) {
+            if (s.fold_scratch[team]) (void) hipFree(s.fold_scratch[team]);  // synchronises the device
+            s.fold_scratch[team] = nullptr;
+            s.fold_scratch_bytes[team] = 0;
+            const size_t sz = std::max<size_t>(need, 1u << 20);
+            if (hipMalloc((void **) &s.fold_scratch[team], sz) != hipSuccess) {
+                (void) hipGetLastError();
+                s.fold_scratch[team] = nullptr;
+                // Failing is safer than a different path from the peers' (they time out in the
+                // start barrier and report it).
+                return fail("reduce: in-place fold scratch of " + std::to_string(sz) + " bytes not allocated");
+            }
+            s.fold_scratch_bytes[team] = sz;
+        }
+        if (s.fold_scratch[team]) scratch = s.fold_scratch[team] + (d0 & 15);
+    }
+    const bool inplace_fold = scratch != nullptr;
+    const bool direct = (fold_size && disjoint && (pl.vec || realign)) || inplace_fold;
     if ((pl.vec || realign) && (direct || (long long) nb >= s.phased_min)) {
         // From phased_min bytes: barrier, one-shot reduce-scatter, barrier, one-shot all-gather,
         // barrier (kernels_impl.h, "Phased reduce-scatter + all-gather").  The barriers carry *ret.
@@ -864,6 +898,7 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         ph.me = t.my_idx;
         ph.peer_nt = s.phased_peer_nt;
         ph.whole = direct ? 1 : 0;
+        if (inplace_fold) ph.dst = scratch;
         if (realign) {
             const uint64_t h = std::min<uint64_t>(n, ((16 - d0 % 16) % 16) / es);
             ph.head = h;
@@ -893,6 +928,7 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         if (mark(4)) return 1;
         if (team_barrier(s, team, a, st)) return 1;
         if (mark(5)) return 1;
+        if (inplace_fold && launch_copy(dst, scratch, nb, st)) return 1;
         s.phase_recorded = s.phase_recorded || ev;
         return 0;
     }
@@ -2126,6 +2162,11 @@ int ishmemi_c_finalize(void)
     (void) hipFree(s.flags);
     (void) hipHostFree(s.err_host);
     (void) hipFree(s.dctx);
+    for (int t = 0; t < kMaxTeams; ++t) {
+        if (s.fold_scratch[t]) (void) hipFree(s.fold_scratch[t]);
+        s.fold_scratch[t] = nullptr;
+        s.fold_scratch_bytes[t] = 0;
+    }
     (void) hipFree(s.dev_epochs);
     (void) hipFree(s.kern_ep);
     s.kern_ep = nullptr;
@@ -2837,6 +2878,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "collect_realign") set_collect_realign((int) (value != 0));
     else if (n == "ar_shifted") s.ar_shifted = value != 0;  // measurement: set alike on every PE
     else if (n == "direct_p2") s.direct_p2 = value != 0;  // measurement: set alike on every PE
+    else if (n == "direct_inplace") s.direct_inplace = value != 0;  // measurement: set alike on every PE
     else if (n == "block_spin") s.block_spin = (int) std::min<long long>(std::max<long long>(value, 0), 2);
     else if (n == "direct_max_pes") s.direct_max_pes = (int) std::min<long long>(std::max<long long>(value, 2), kMaxPes);
     else if (n == "phase_unaligned") set_phase_unaligned((int) (value != 0));
@@ -2887,6 +2929,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "collect_realign") return collect_realign();
     if (n == "ar_shifted") return s.ar_shifted;
     if (n == "direct_p2") return s.direct_p2;
+    if (n == "direct_inplace") return s.direct_inplace;
     if (n == "block_spin") return s.block_spin;
     if (n == "direct_max_pes") return s.direct_max_pes;
     if (n == "phase_unaligned") return phase_unaligned();
