@@ -284,7 +284,8 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
  * 0: narrow items), "barrier_kind" (0 kernel, 1 stream memory operations), "block_spin" (blocking
  * calls' wait: 2, default, spin on a stream-written host word; 1 the spin then
  * hipStreamSynchronize; 0 hipStreamSynchronize), "direct_max_pes" (largest team taking the
- * whole-array fold, default 4).  "ll_max_bytes",
+ * whole-array fold, default 4), "direct_inplace" (1, default: in-place calls with p * B <= 4 MiB
+ * fold into a team-private scratch and copy back).  "ll_max_bytes",
  * "oneshot_p2_max_bytes" and "phased_min_bytes" choose the kernels of a multi-PE call: init
  * agrees on them (the minimum over the PEs; the maximum for "phased_min_bytes") and a later
  * set_param must be made with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,
