@@ -115,11 +115,13 @@ def pmc_traffic(kernel_tag: str, nbytes: int):
     return None
 
 
-def multi_pe_kernel(B: int, phased_min: int, world: int = 0, oneshot_p2: int = -1) -> str:
+def multi_pe_kernel(B: int, phased_min: int, world: int = 0, fold_limit: int = -1) -> str:
     """The multi-PE kernels a B-byte f32 sum with disjoint buffers takes (runtime.cpp reduce_heap):
-    two members up to oneshot_p2 bytes fold the whole array between two barriers; the phased path's
-    one-shot grids for payloads of at least phased_min bytes (-1: off); else the persistent kernel."""
-    if (world == 2 and 0 <= B <= oneshot_p2) or (3 <= world <= 4 and 0 <= (world - 1) * B <= oneshot_p2 // 4):
+    up to the team's fold bound (get_param "fold_limit_bytes": path_limits, by topology; 0 for
+    teams of more than 4) every member folds the whole array between two barriers; the phased
+    path's one-shot grids for payloads of at least phased_min bytes (-1: off); else the persistent
+    kernel."""
+    if world >= 2 and 0 <= B <= fold_limit:
         return (f"rs_phase_kernel<float,SUM,{world}> whole-array fold on every member between 2 one-workgroup "
                 "team barriers")
     if phased_min >= 0 and B >= phased_min:
@@ -239,7 +241,7 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max, share: int = 
     min / max winner rotating over the PEs)."""
     from ishmem_amd import selfcheck as sc
     out = []
-    phased_min, oneshot_p2 = ish.get_param("phased_min_bytes"), ish.get_param("oneshot_p2_max_bytes")
+    phased_min, fold_limit = ish.get_param("phased_min_bytes"), ish.get_param("fold_limit_bytes")
     for dtn, npd in (("int32", np.int32), ("double", np.float64)):
         es = np.dtype(npd).itemsize
         nmax = nbytes_max // es
@@ -281,7 +283,7 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max, share: int = 
                 bad = sum(sc.count_wrong(hip, dst, op, npd, world, lo, m) for lo, m in wins)
                 bad = int(max_over_ranks(dist, [float(bad)])[0])
                 _, t_roof = roofline(world, share, nb, us * 1e-3,
-                                     multi_pe_kernel(nb, phased_min, world, oneshot_p2))
+                                     multi_pe_kernel(nb, phased_min, world, fold_limit))
                 out.append({"op": op, "dtype": dtn, "bytes": nb, "us": round(us, 2),
                             "algbw_GiBps": round(nb / GiB / (us * 1e-6), 2),
                             # t_roof / t: the same bound as the line's roofline (xGMI links one PE
@@ -295,34 +297,6 @@ def config5_sweep(ish, hip, world, rank, dist, stream, nbytes_max, share: int = 
     return out
 
 
-def stream_barrier_probe(ish, hip, dist, stream, limit_s: float = 20.0) -> bool:
-    """One stream-memory-op team barrier (ISHMEM_BARRIER_KIND=stream) on every rank before the
-    tuning leg times them: that barrier has no timeout, and it has never run between two GPUs, so a
-    barrier that does not complete within limit_s on some rank is released on every rank
-    (set_param "stream_barrier_release" stores the awaited epoch into the rank's own wait row) and
-    the rows are skipped — the leg must not hang the measured line."""
-    import time as _t
-    old = ish.get_param("barrier_kind")
-    ish.set_param("barrier_kind", 1)
-    try:
-        if ish.team_sync_on_stream(0, None, stream) != 0:
-            done = False
-        else:
-            t0 = _t.monotonic()
-            done = hip.stream_query(stream)
-            while not done and _t.monotonic() - t0 < limit_s:
-                _t.sleep(0.01)
-                done = hip.stream_query(stream)
-        stuck = max_over_ranks(dist, [0.0 if done else 1.0])[0] > 0
-        if stuck:
-            ish.set_param("stream_barrier_release", 0)
-            hip.stream_synchronize(stream)
-            dist.barrier()
-        return not stuck
-    finally:
-        ish.set_param("barrier_kind", old)
-
-
 def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     """N>1: the f32 sum again under other launch shapes, set alike on every rank, so the driver's
     multi-GPU run records how the xGMI path responds (data for choosing the defaults; one
@@ -334,9 +308,6 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
                between barriers) and on the persistent kernel (the phased threshold, 4 MiB);
       phased_peer_nt - 64 MiB and the payload on the phased path with nontemporal peer loads
                (the collectives issue sc0 sc1 ones; the tripwire_peer_nt leg checks coherence);
-      barrier_kernel / barrier_stream - the phased path at 1 / 4 / 16 MiB and the payload with its
-               three team barriers as the one-workgroup barrier kernel (default) or as stream
-               memory operations (ISHMEM_BARRIER_KIND=stream: the command processor waits);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
       fold  - 512 KiB - 4 MiB: the whole-array fold between two barriers forced for this team
               size against the path without it (granule path off in both);
@@ -375,43 +346,97 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
         out.append({"case": case, **params, "bytes": nbytes, "us": round(ms * 1e3, 2),
                     "algbw_GiBps": round(nbytes / GiB / (ms * 1e-3), 2)})
 
+    # Rows that time reduce-scatter + all-gather turn the whole-array fold off (co-located bound
+    # oneshot_p2, cross-device bound xgmi_fold_max_bytes: runtime.cpp path_limits).
+    no_fold = {"oneshot_p2_max_bytes": 0, "xgmi_fold_max_bytes": 0}
     for ws in (4, 8, 16, 32):
         for nb in (1 << 20, 4 << 20, 16 << 20):
             if nb <= B:
-                run("wait", "wait_slots", ws, nb, 20, also={"phased_min_bytes": -1})
+                run("wait", "wait_slots", ws, nb, 20, also={"phased_min_bytes": -1, **no_fold})
     for nb in sorted({2 << 20, 4 << 20, 8 << 20, 16 << 20, 64 << 20, B}):
         if nb <= B:
-            run("phased", "phased_min_bytes", 0, nb, 5 if nb == B else 20)
-            run("persistent", "phased_min_bytes", -1, nb, 5 if nb == B else 20)
+            run("phased", "phased_min_bytes", 0, nb, 5 if nb == B else 20, also=no_fold)
+            run("persistent", "phased_min_bytes", -1, nb, 5 if nb == B else 20, also=no_fold)
     for nb in sorted({64 << 20, B}):
         if nb <= B:  # the phased grids' peer loads nontemporal instead of sc0 sc1 (measurement only)
-            run("phased_peer_nt", "phased_peer_nt", 1, nb, 5 if nb == B else 20, also={"phased_min_bytes": 0})
-    if stream_barrier_probe(ish, hip, dist, stream):
-        for nb in sorted({1 << 20, 4 << 20, 16 << 20, B}):
-            if nb <= B:  # set alike on every rank (the two kinds use different flag rows)
-                for kind, case in ((0, "barrier_kernel"), (1, "barrier_stream")):
-                    run(case, "barrier_kind", kind, nb, 5 if nb == B else 20, also={"phased_min_bytes": 0})
-    else:
-        out.append({"case": "barrier_stream", "error": "a probe stream barrier did not complete within 20 s on "
-                                                        "some rank; released (set_param stream_barrier_release)"})
+            run("phased_peer_nt", "phased_peer_nt", 1, nb, 5 if nb == B else 20, also={"phased_min_bytes": 0, **no_fold})
     if world == 2:
-        run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5)
-        run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5)
+        run("p2_oneshot", "oneshot_p2_max_bytes", 1 << 40, B, 5, also={"xgmi_fold_max_bytes": 1 << 40})
+        run("p2_rs_ag", "oneshot_p2_max_bytes", 0, B, 5, also={"xgmi_fold_max_bytes": 0})
     # The whole-array fold (two barriers around one grid in which every member folds every
     # member's source) against the default path below it, at mid sizes: decided on one GPU for
     # 2-4 PEs; over xGMI each member pulls (p - 1) * B instead of 2(p - 1)/p * B.
     for nb in (512 << 10, 1 << 20, 2 << 20, 4 << 20):
         if nb <= B:
             run("fold", "direct_max_pes", max(2, world), nb, 20,
-                also={"direct_p2": 1, "oneshot_p2_max_bytes": 1 << 40, "ll_max_bytes": 0})
+                also={"direct_p2": 1, "oneshot_p2_max_bytes": 1 << 40, "xgmi_fold_max_bytes": 1 << 40,
+                      "ll_max_bytes": 0})
             run("no_fold", "direct_p2", 0, nb, 20, also={"ll_max_bytes": 0})
     cap = int(ish.get_param("ll_capacity_bytes"))  # the ring's capacity at this team size (the leg
     # times the granule path up to it, past the default threshold ll_limit_bytes where that is lower)
     for nb in (4096, 16384, 65536, 131072, 262144, 524288):
         if nb <= cap:
-            run("ll_on", "ll_max_bytes", cap, nb, 50)
+            run("ll_on", "ll_max_bytes", cap, nb, 50, also={"xgmi_ll_max_bytes": cap})
             run("ll_off", "ll_max_bytes", 0, nb, 50)
     return out
+
+
+def recommended(rows: list, world: int, share: int, B: int) -> dict:
+    """The path thresholds the xgmi_tuning rows measured, as the environment
+    a run on this topology would set, so the node run yields its defaults directly:
+      granule path - the largest size up to which ll_on beat ll_off at every measured size;
+      fold         - the largest size up to which the whole-array fold beat the path without it at
+                     every measured size (2 PEs: past 4 MiB when p2_oneshot also beat p2_rs_ag at B);
+      phased       - the smallest size from which phased beat persistent at every larger size.
+    share == 1 (one PE per GPU): the cross-device variables (ISHMEM_XGMI_*, runtime.cpp
+    path_limits); co-located PEs: the variables of round 5's co-located crossovers."""
+    def us(case, nb):
+        for r in rows:
+            if r.get("case") == case and r.get("bytes") == nb and "us" in r:
+                return r["us"]
+        return None
+
+    def prefix_limit(a_case, b_case):
+        lim, pairs = 0, []
+        for nb in sorted({r["bytes"] for r in rows if r.get("case") == a_case}):
+            a, b = us(a_case, nb), us(b_case, nb)
+            if a is None or b is None:
+                break
+            pairs.append([nb, a, b])
+            if a >= b:
+                break
+            lim = nb
+        return lim, pairs
+
+    env, basis = {}, {}
+    cross = share == 1
+    ll, basis["ll_on_vs_ll_off_us"] = prefix_limit("ll_on", "ll_off")
+    env["ISHMEM_XGMI_LL_MAX_BYTES" if cross else "ISHMEM_LL_MAX_BYTES"] = ll
+    fold, basis["fold_vs_no_fold_us"] = prefix_limit("fold", "no_fold")
+    fold_sizes = [p[0] for p in basis["fold_vs_no_fold_us"]]
+    if world == 2 and fold_sizes and fold == fold_sizes[-1]:
+        a, b = us("p2_oneshot", B), us("p2_rs_ag", B)
+        basis["p2_oneshot_vs_rs_ag_us_at_payload"] = [B, a, b]
+        if a is not None and b is not None and a < b:
+            fold = B
+    if world <= 4:
+        if cross:
+            env["ISHMEM_XGMI_FOLD_MAX_BYTES"] = fold
+        else:  # co-located: 2 members fold up to oneshot_p2, 3-4 up to oneshot_p2 / 4 / (p - 1)
+            env["ISHMEM_ONESHOT_P2_MAX_BYTES"] = fold if world == 2 else fold * 4 * (world - 1)
+    thr, pp = None, []
+    for nb in sorted({r["bytes"] for r in rows if r.get("case") == "phased"}, reverse=True):
+        a, b = us("phased", nb), us("persistent", nb)
+        if a is None or b is None:
+            break
+        pp.append([nb, a, b])
+        if a >= b:
+            break
+        thr = nb
+    basis["phased_vs_persistent_us"] = sorted(pp)
+    env["ISHMEM_PHASED_MIN_BYTES"] = thr if thr is not None else -1
+    return {"env": env, "basis": basis, "topology": "one PE per GPU (cross-device teams)" if cross
+            else f"{share} PEs per GPU (co-located teams)"}
 
 
 def link_topology(hip, device: int, world: int) -> list | dict:
@@ -864,7 +889,7 @@ def main() -> int:
     share = int(ish.get_param("device_share")) if world > 1 else 1
     roof, t_roof = roofline(world, share, B, kern_ms,
                             multi_pe_kernel(B, ish.get_param("phased_min_bytes"), world,
-                                            ish.get_param("oneshot_p2_max_bytes")) if world > 1 else "")
+                                            ish.get_param("fold_limit_bytes")) if world > 1 else "")
     algbw_roof = B / GiB / t_roof
     targets = {"algbw_roofline_GiBps": algbw_roof, "algbw_frac_of_roofline": algbw / algbw_roof}
     if algbw > algbw_roof:
@@ -927,6 +952,7 @@ def main() -> int:
         log("launch-shape sweep")
         try:
             extra["xgmi_tuning"] = xgmi_tuning(ish, hip, src, dst, B, world, dist, stream)
+            extra["recommended"] = recommended(extra["xgmi_tuning"], world, share, B)
         except Exception as ex:
             extra["xgmi_tuning"] = {"error": str(ex)}
 

@@ -240,7 +240,9 @@ int ishmemi_c_stream_record_event(void *stream, void *done);
  * which the user passes to its kernel and on to the header-only device API (ishmemx_device.h).
  * Layout is part of the ABI. */
 #define ISHMEMI_C_MAX_PES 16
-#define ISHMEMI_C_MAX_TEAMS 16
+/* Team slots: the reference's ISHMEM_TEAMS_MAX default and cap (src/ishmem/env_defs.h:34,
+ * src/teams.cpp:245-248); ISHMEM_TEAMS_MAX (3..64) lowers the number in use. */
+#define ISHMEMI_C_MAX_TEAMS 64
 #define ISHMEMI_C_DEV_PHASES 4
 typedef struct {
     int32_t pe, npes;
@@ -307,6 +309,13 @@ size_t ishmemi_c_dtype_size(int dtype);
 int ishmemi_c_op_dtype_valid(int op, int dtype);
 /* Partition used by the multi-PE schedule: items of member `c` out of `nitems` (test hook). */
 int ishmemi_c_chunk_bounds(uint64_t nitems, int npes, int c, uint64_t *begin, uint64_t *end);
+/* Path thresholds of a team of `npes` members (no reference counterpart; no GPU needed): payloads
+ * up to *ll_limit bytes take the granule path, disjoint payloads up to *fold_limit the whole-array
+ * fold between two barriers (0: never).  colocated != 0: every member on one GPU (round 5's
+ * measured crossovers); 0: members on different GPUs (the link-byte model of runtime.cpp
+ * path_limits, or ISHMEM_XGMI_LL_MAX_BYTES / ISHMEM_XGMI_FOLD_MAX_BYTES).  Computed with the
+ * current parameters (the defaults before init). */
+int ishmemi_c_path_limits(int npes, int colocated, long long *ll_limit, long long *fold_limit);
 /* Native bootstrap self-test (no GPU needed): allgather of one int per PE + barrier.
  * Fills out[npes]; used by the multi-process CPU tests. */
 int ishmemi_c_bootstrap_selftest(int pe, int npes, const char *key, int value, int *out);

@@ -74,6 +74,7 @@ PROTOTYPES = [
     ("ishmemi_c_dtype_size", _sz, [_i]),
     ("ishmemi_c_op_dtype_valid", _i, [_i, _i]),
     ("ishmemi_c_chunk_bounds", _i, [_u64, _i, _i, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    ("ishmemi_c_path_limits", _i, [_i, _i, ctypes.POINTER(_ll), ctypes.POINTER(_ll)]),
     ("ishmemi_c_bootstrap_selftest", _i, [_i, _i, ctypes.c_char_p, _i, ctypes.POINTER(_i)]),
     ("ishmemi_c_version", ctypes.c_char_p, []),
 ]

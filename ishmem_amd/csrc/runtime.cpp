@@ -30,16 +30,38 @@
 namespace ishmemi {
 namespace {
 
+// Team slots: the reference's table size, ISHMEM_TEAMS_MAX (default 64, src/ishmem/env_defs.h:34),
+// capped at 64 by its 64-bit slot mask (src/teams.cpp:245-248) — as here, where the free-slot mask
+// agreed at split is a u64.  Slots 0-2 are WORLD, SHARED and NODE.
 constexpr int kMaxTeams = ISHMEMI_C_MAX_TEAMS;
+constexpr int kPredefTeams = ISHMEMI_C_TEAM_NODE + 1;
+constexpr int kTeamsMaxDefault = 64;
+static_assert(kMaxTeams == 64, "the split's free-slot mask is a u64");
 static_assert(kMaxPes == ISHMEMI_C_MAX_PES, "device ctx layout");
-// Device-API flags ([team][phase][pe] u32) follow the host-launch flag blocks in the same
-// fine-grained, IPC-shared allocation.
+// Device-API flags ([team][phase][pe] u32, 256 B per slot).
 constexpr size_t kDevFlagWordsPerTeam = (size_t) ISHMEMI_C_DEV_PHASES * kMaxPes;
 constexpr size_t kDevFlagBytes = (size_t) kMaxTeams * kDevFlagWordsPerTeam * 4;
-// Small-message rings (kernels.h: kLLTeamBytes per team) follow, 256-B aligned.
-constexpr size_t kLLOffset = ((size_t) kMaxTeams * kTeamFlagBytes + kDevFlagBytes + 255) & ~(size_t) 255;
-constexpr size_t kFlagAllocBytes = kLLOffset + (size_t) kMaxTeams * kLLTeamBytes;
+// Base flag block, allocated and IPC-exported at init (round 6): the predefined teams' flag blocks
+// (kernels.h kTeamFlagBytes each), the device-API flags of every slot, then the predefined teams'
+// small-message rings (kLLTeamBytes each), 256-B aligned.  A team created by a split gets a block
+// of its own (kTeamAllocBytes: flag block + ring), allocated and exchanged among its members at the
+// split and freed at destroy (TeamMem), so a PE holds (and peers map) blocks only for teams that
+// exist.  Round 5 reserved flag block + ring for 16 slots at init: 132 MiB per PE whatever the
+// teams (kRound5FlagBytes, for get_param "flag_block_bytes" comparisons).
+constexpr size_t kBaseDevOffset = (size_t) kPredefTeams * kTeamFlagBytes;
+constexpr size_t kBaseLLOffset = (kBaseDevOffset + kDevFlagBytes + 255) & ~(size_t) 255;
+constexpr size_t kBaseAllocBytes = kBaseLLOffset + (size_t) kPredefTeams * kLLTeamBytes;
+constexpr size_t kTeamLLOffset = (kTeamFlagBytes + 255) & ~(size_t) 255;
+constexpr size_t kTeamAllocBytes = kTeamLLOffset + kLLTeamBytes;
+constexpr size_t kRound5FlagBytes = (((size_t) 16 * kTeamFlagBytes + 16 * kDevFlagWordsPerTeam * 4 + 255) & ~(size_t) 255) +
+                                    (size_t) 16 * kLLTeamBytes;
+// In-place whole-array fold (reduce_heap): while p * B <= this, into a team-private scratch of
+// kInplaceFoldBytes / p + 256 bytes, allocated when the team is created.
+constexpr uint64_t kInplaceFoldBytes = 4u << 20;
 constexpr size_t kHeapAlign = 256;
+// Symmetric scratch of the team-management collectives (split's slot mask and handle exchange).
+constexpr size_t kTeamScratchBytes = 4096;
+constexpr size_t kSplitRecBytes = 128;  // one member's record in the split's handle exchange
 // Offset of team_exchange's arrays in the host-mapped error-word allocation (after the words).
 constexpr size_t kErrExchOffset = ((kMaxTeams + 1) * sizeof(uint32_t) + 63) & ~(size_t) 63;
 // Completion word of the blocking calls' host wait (host_wait), on its own line.
@@ -215,6 +237,34 @@ bool env_flag_true(const char *name)
     return s && *s && !env_flag_false(name);
 }
 
+// ISHMEM_* variables this library reads (runtime, launcher identity, build, tests) or accepts from
+// the reference's list (src/ishmem/env_defs.h; the ones this path has no use for are read and
+// ignored, as a drop-in must start under the reference's job scripts).  Any other ISHMEM_* name
+// gets the reference's warning at init (src/env_utils.cpp:193-196), not an error.
+void warn_unknown_env()
+{
+    static const char *const known[] = {
+        // the reference's (src/ishmem/env_defs.h)
+        "DEBUG", "ENABLE_VERBOSE_PRINT", "STACK_PRINT_LIMIT", "ENABLE_GPU_IPC", "ENABLE_GPU_IPC_PIDFD",
+        "SYMMETRIC_SIZE", "ENABLE_ACCESSIBLE_HOST_HEAP", "NBI_COUNT", "MWAIT_BURST", "SHMEM_LIB_NAME",
+        "MPI_LIB_NAME", "PMI_LIB_NAME", "TEAMS_MAX", "TEAM_SHARED_ONLY_SELF", "RUNTIME", "RUNTIME_USE_OSHMPI", "ROOT",
+        // this library's
+        "PE", "NPES", "DEVICE", "BOOTSTRAP_KEY", "TIMEOUT_MS", "MAX_BLOCKS", "WAIT_SLOTS", "LL_MAX_BYTES",
+        "ONESHOT_P2_MAX_BYTES", "PHASED_MIN_BYTES", "PHASED_PEER_NT", "STAGING_SIZE", "STAGING_SLOTS",
+        "STAGED_COPY_KERNEL", "STREAM_ORDER", "FLAGS_KIND", "EP_UNCACHED", "BARRIER_KIND", "XGMI_LL_MAX_BYTES",
+        "XGMI_FOLD_MAX_BYTES", "TEST_FLAGS_UNAVAILABLE", "TEST_PCI_BUS",
+        // the Python package, build and bench harness
+        "AMD_LIB", "OFFLOAD_ARCH", "BENCH_SAME_DEVICE"};
+    for (char **e = ::environ; e && *e; ++e) {
+        if (strncmp(*e, "ISHMEM_", 7) != 0) continue;
+        const char *name = *e + 7, *eq = strchr(name, '=');
+        const size_t len = eq ? (size_t) (eq - name) : strlen(name);
+        bool ok = false;
+        for (const char *k : known) ok = ok || (strlen(k) == len && strncmp(k, name, len) == 0);
+        if (!ok) fprintf(stderr, "[ishmem_amd] WARN: Environment variable 'ISHMEM_%.*s' is not a supported variable\n", (int) len, name);
+    }
+}
+
 // Lowest ISHMEM_WAIT_SLOTS / set_param("wait_slots") accepted: the process's hardware queue count.
 long long wait_slots_floor() { return std::max<long long>(1, env_ll("GPU_MAX_HW_QUEUES", 4)); }
 
@@ -223,6 +273,22 @@ struct Team {
     int start = 0, stride = 1, size = 1;  // in world PEs (src/teams.h:56-76)
     int my_idx = -1;                      // my index in the team, -1 if not a member
     int num_contexts = 0;                 // ishmem_team_config_t given at split (reported only)
+    // Every member on one device (co-located PEs: tests, rehearsals) or not (one PE per GPU over
+    // xGMI): picks the path thresholds (path_limits).  The same on every member (from the
+    // device identities allgathered at init).
+    bool colocated = true;
+};
+
+// Memory of a team slot on this PE (round 6).  Predefined teams point into the base block; a
+// split team's own block (flag block + ring) and the imported blocks of its other members are
+// released by destroy.
+struct TeamMem {
+    uint32_t *flags[kMaxPes] = {};  // the team's flag block on world PE j, mapped here (members only)
+    uint64_t *ring[kMaxPes] = {};   // the team's small-message ring on world PE j
+    void *own = nullptr;            // this PE's block of a split team
+    void *imported[kMaxPes] = {};   // members' blocks opened over IPC (split teams)
+    char *fold_scratch = nullptr;   // in-place whole-array fold (kInplaceFoldBytes / p + 256 B)
+    size_t fold_scratch_bytes = 0;
 };
 
 constexpr long long kPhasedOff = std::numeric_limits<long long>::max();
@@ -253,7 +319,7 @@ struct PeRecord {
     int64_t max_blocks, ll_max_bytes, oneshot_p2, phased_min;
     uint64_t staging_bytes;
     int64_t staging_slots;
-    int32_t barrier_kind, pad_;
+    int64_t xgmi_ll_max, xgmi_fold_max;  // path_limits overrides for cross-device teams (-1: model)
     hipIpcMemHandle_t heap_handle;
     hipIpcMemHandle_t flags_handle;
 };
@@ -270,9 +336,13 @@ struct State {
     std::map<size_t, size_t> used;       // offset -> bytes
     char *peer_heap[kMaxPes] = {};
 
-    uint32_t *flags = nullptr;  // kMaxTeams flag blocks (+ LL rings), see FlagMem
-    int flags_kind = 0;         // FlagMem of the block in use
-    uint32_t *peer_flags[kMaxPes] = {};
+    uint32_t *flags = nullptr;  // base flag block (predefined teams, device-API flags), see FlagMem
+    int flags_kind = 0;         // FlagMem of the base block; split teams' blocks take the same kind
+    uint32_t *peer_flags[kMaxPes] = {};  // every PE's base block, mapped here
+    int dev_id[kMaxPes] = {};            // world PE j's device, as an index into the job's devices
+    TeamMem tmem[kMaxTeams];
+    int teams_max = kTeamsMaxDefault;    // ISHMEM_TEAMS_MAX: slots [0, teams_max) are used
+    size_t team_block_bytes = 0;         // split teams' blocks this PE holds (get_param "flag_block_bytes")
     uint32_t *err_host = nullptr;  // host-mapped error words, one per team (+1: device API)
     uint32_t *err_dev = nullptr;
     // Host-mapped coherent [2][kMaxPes] u64 (same allocation as err_host): team_exchange's arrays.
@@ -328,17 +398,13 @@ struct State {
     // barrier (1, default) or the persistent kernel's one-shot mode (0; set_param "direct_p2",
     // alike on every PE).
     int direct_p2 = 1;
-    int direct_max_pes = 4;
+    int direct_max_pes = 4;  // the whole-array fold up to this team size (set_param "direct_max_pes", >= 2)
     int direct_inplace = 1;
-    char *fold_scratch[kMaxTeams] = {};  // in-place whole-array fold: team-private device scratch
-    size_t fold_scratch_bytes[kMaxTeams] = {};  // the whole-array fold up to this team size (set_param "direct_max_pes", >= 2)
-    // Team barriers of the phased paths and ishmem_team_sync: 0 = the one-workgroup barrier
-    // kernel (team_sync_kernel), 1 = stream memory operations (ISHMEM_BARRIER_KIND=stream: the
-    // command processor waits, no workgroup is held; team_barrier).  Agreed at init; sb_epoch is
-    // the stream barrier's per-team epoch, counted on the host (every member calls the same
-    // collectives of a team in the same order) and reset with the team's flag block.
-    int barrier_kind = 0;
-    uint32_t sb_epoch[kMaxTeams] = {};
+    // Cross-device teams' thresholds (path_limits): -1 = the link-byte model's; ISHMEM_XGMI_LL_MAX_BYTES /
+    // ISHMEM_XGMI_FOLD_MAX_BYTES (agreed at init) or set_param override them, e.g. with the crossovers
+    // the N > 1 bench line's `recommended` block measured on the node.
+    long long xgmi_ll_max = -1, xgmi_fold_max = -1;
+    double xgmi_link_bps = 76.8e9;  // per link and direction (set_param "xgmi_link_mbps")
     hipEvent_t ev_in[kMaxStagingSlots] = {}, ev_red[kMaxStagingSlots] = {}, ev_out[kMaxStagingSlots] = {};
 
     Team teams[kMaxTeams];
@@ -351,7 +417,12 @@ struct State {
     // Measurement hook (set_param "phase_events"): events around the phased reduce's launches.
     bool phase_events = false, phase_recorded = false;
     hipEvent_t phase_ev[6] = {};
+    // Init phase durations (us), printed under ISHMEM_DEBUG=2 and read by get_param("init_us_<phase>").
+    double init_us[8] = {};
 };
+
+// Init phases timed (State::init_us): names for the debug line and get_param.
+const char *const kInitPhase[8] = {"hip", "heap", "flags", "bootstrap", "ipc_heap", "ipc_flags", "teams", "total"};
 
 State &S()
 {
@@ -400,16 +471,19 @@ char *translate(const State &s, const void *p, int pe)
     return s.peer_heap[pe] + ((const char *) p - s.heap);
 }
 
-uint64_t *ll_ring(uint32_t *flags_base, int team)
-{
-    return flags_base ? (uint64_t *) ((char *) flags_base + kLLOffset + (size_t) team * kLLTeamBytes)
-                      : nullptr;
-}
-
-uint32_t *team_flags(uint32_t *base, int team)
+// A predefined team's flag block / ring inside a base block (own or a peer's, mapped here).
+uint32_t *base_team_flags(uint32_t *base, int team)
 {
     return base ? base + (size_t) team * (kTeamFlagBytes / 4) : nullptr;
 }
+
+uint64_t *base_team_ring(uint32_t *base, int team)
+{
+    return base ? (uint64_t *) ((char *) base + kBaseLLOffset + (size_t) team * kLLTeamBytes) : nullptr;
+}
+
+// The device-API flag rows of every slot, in a base block.
+uint32_t *dev_flags(uint32_t *base) { return base ? base + kBaseDevOffset / 4 : nullptr; }
 
 // ---------------- symmetric heap allocator (deterministic first fit, same on every PE) -------
 void *heap_alloc(State &s, size_t bytes, size_t align)
@@ -532,12 +606,12 @@ int team_args(State &s, int team, ReduceArgs &a, std::string &why)
     memset(&a, 0, sizeof(a));
     a.p = t.size;
     a.me = t.my_idx;
-    a.my_flags = team_flags(s.flags, team);
+    a.my_flags = s.tmem[team].flags[s.pe];
     a.err = s.err_dev + team;
     a.timeout_ticks = (uint64_t) s.timeout_ms * 100000ull;  // s_memrealtime runs at 100 MHz
     for (int j = 0; j < t.size; ++j) {
         const int gpe = t.start + j * t.stride;
-        a.peer_flags[j] = team_flags(s.peer_flags[gpe], team);
+        a.peer_flags[j] = s.tmem[team].flags[gpe];
         if (!a.peer_flags[j]) {
             why = "team member " + std::to_string(gpe) + " has no mapped flag block";
             return 1;
@@ -617,27 +691,89 @@ int launch_copy(void *dst, const void *src, size_t bytes, hipStream_t st)
     return 0;
 }
 
-// Small payloads (<= the team's ring capacity, kernels.h ll_capacity, and <= ll_max_bytes; device
-// memory anywhere, any element-aligned address — the kernel picks 8-, 4- or 1-byte accesses,
-// ll_load / ll_store): one-hop push of {data, epoch} granules into the peers' rings, no barriers
-// (ll_kernel).  The choice depends on the byte count and the team size only, which every member
-// shares.
-// Teams that take the whole-array fold (3 or 4 members, reduce_heap "direct") leave it the sizes
-// from 768 KiB / p: the fold costs a flat ~9-10 us at 256 KiB - 2 MiB on one GPU where the granule
-// path grows with p (4 PEs: 11.0-11.6 us at 256 KiB, 15.1-15.6 at 512 KiB; 3 PEs: 9.0-9.3 / 12.1;
-// profiles/r05/direct_p2/r05zzd_ab.txt).
-size_t ll_limit(const State &s, int p)
+// ---------------- path thresholds (round 6: per team, by topology) ---------------------------
+// Two thresholds pick a multi-PE reduce's path below the phased one (phased_min):
+//   ll    - payloads up to it take the granule path (ll_kernel: one push of {data, epoch} granules
+//           into every peer's ring, no barriers; 2 link bytes per payload byte, the granules
+//           carry 4 B of payload in 8);
+//   fold  - disjoint payloads up to it, on teams of 2 .. direct_max_pes members, take the
+//           whole-array fold between two barriers (every member pulls every peer's whole source:
+//           B per link) instead of reduce-scatter + all-gather (2B / p per link).
+// Co-located teams (every member on one GPU: tests, rehearsals) keep round 5's measured
+// crossovers: ll = min(ll_max_bytes, ring capacity), and 768 KiB / p for
+// 3-4-member teams, where the fold's flat ~9-10 us beat the granules; fold = oneshot_p2 at 2
+// members, oneshot_p2 / 4 / (p - 1) at 3-4 (each member reads (p - 1) B).  Those were measured
+// where link bytes are free (all PEs on one HBM), so teams whose members sit on different GPUs
+// (one PE per GPU over xGMI) take them from a link-byte model instead:
+//   t_ll(B)   = a_ll(p)   + 1 hop  + 2B / L
+//   t_fold(B) = a_fold(p) + 2 hops + B / L        (two barriers)
+//   t_rsag(B) = a_rsag(p) + 3 hops + 2B / (p L)   (start / segment / done handshakes)
+// L = xgmi_link_bps per link and direction (76.8 GB/s: the brief's 153.6 GB/s per link read as
+// both directions together), a hop = one fabric round trip (kHopUs, assumed: never measured
+// between GPUs here), a_*(p) = the fixed costs measured with one-PE-per-GPU launch shapes on one
+// GPU in round 5 (the granule path 4.1-4.6 us at 2 PEs, 5.5-6.3 at 4; the fold 9.5 / 10.0-10.6 /
+// 11.3-12.5 us at 2 / 3 / 4; the persistent kernel 9.6-10.2 / 13.8-14.1 / 16-17).
+// Each threshold is the crossover of two lines, so it is closed-form.  ISHMEM_XGMI_LL_MAX_BYTES /
+// ISHMEM_XGMI_FOLD_MAX_BYTES (or set_param "xgmi_ll_max_bytes" / "xgmi_fold_max_bytes") replace
+// the model's values, e.g. with the crossovers the node run's `recommended` block measured.
+constexpr double kHopUs = 1.0;
+constexpr long long kUnlimited = std::numeric_limits<long long>::max();
+struct Line {
+    double a_us, b_us_per_byte;
+};
+Line model_ll(int p, double L) { return {4.5 + 0.5 * (p - 2) + 1 * kHopUs, 2e6 / L}; }
+Line model_fold(int p, double L) { return {9.0 + 0.75 * (p - 2) + 2 * kHopUs, 1e6 / L}; }
+Line model_rsag(int p, double L) { return {9.5 + 2.5 * (p - 2) + 3 * kHopUs, 2e6 / (p * L)}; }
+
+// Largest payload for which line f is not slower than line g (f steeper or equal), or kUnlimited.
+long long crossover(const Line &f, const Line &g)
 {
-    size_t lim = std::min<size_t>((size_t) std::max<long long>(s.ll_max_bytes, 0), ll_capacity(p));
-    if (p >= 3 && p <= s.direct_max_pes && s.direct_p2) lim = std::min<size_t>(lim, (768u << 10) / (size_t) p);
-    return lim;
+    if (f.a_us > g.a_us) return 0;
+    if (f.b_us_per_byte <= g.b_us_per_byte) return kUnlimited;
+    return (long long) ((g.a_us - f.a_us) / (f.b_us_per_byte - g.b_us_per_byte));
 }
 
+// ll, fold: as above (fold 0 when the team does not take the fold: direct_p2 off, or more than
+// direct_max_pes members); oneshot: the same bound ungated, for the persistent kernel's two-member
+// one-shot mode (direct_p2 0, or operands without a common 16-B body).
+struct PathLimits {
+    long long ll, fold, oneshot;
+};
+
+PathLimits path_limits(const State &s, int p, bool colocated)
+{
+    PathLimits r{0, 0, 0};
+    if (p < 2) return r;
+    const long long cap = std::min<long long>(std::max<long long>(s.ll_max_bytes, 0), (long long) ll_capacity(p));
+    const bool fold_team = s.direct_p2 && p <= s.direct_max_pes;
+    if (colocated) {
+        r.ll = cap;
+        if (p >= 3 && fold_team) r.ll = std::min<long long>(r.ll, (768ll << 10) / p);
+        r.fold = p == 2 ? s.oneshot_p2 : s.oneshot_p2 / 4 / (p - 1);
+    } else {
+        const double L = s.xgmi_link_bps;
+        long long ll = crossover(model_ll(p, L), model_rsag(p, L));
+        if (fold_team) ll = std::min(ll, crossover(model_ll(p, L), model_fold(p, L)));
+        if (s.xgmi_ll_max >= 0) ll = s.xgmi_ll_max;
+        r.ll = std::min(cap, ll);
+        r.fold = s.xgmi_fold_max >= 0 ? s.xgmi_fold_max : crossover(model_fold(p, L), model_rsag(p, L));
+    }
+    r.oneshot = r.fold;
+    if (!fold_team) r.fold = 0;
+    return r;
+}
+
+PathLimits team_limits(const State &s, const Team &t) { return path_limits(s, t.size, t.colocated); }
+
+// Small payloads (<= the team's ll threshold; device memory anywhere, any element-aligned address
+// — the kernel picks 8-, 4- or 1-byte accesses, ll_load / ll_store): one-hop push of {data, epoch}
+// granules into the peers' rings, no barriers (ll_kernel).  The choice depends on the byte count
+// and the team only, which every member shares.
 bool ll_eligible(const State &s, const Team &t, const void *dst, const void *src, size_t bytes)
 {
     (void) dst;
     (void) src;
-    return t.size > 1 && bytes > 0 && bytes <= ll_limit(s, t.size);
+    return t.size > 1 && bytes > 0 && (long long) bytes <= team_limits(s, t).ll;
 }
 
 // Collectives of one PE run in the order they were called, whatever streams they were enqueued
@@ -692,31 +828,18 @@ int host_wait(State &s, hipStream_t st)
 }
 
 // Team barrier on `st`, stream ordered (everything before it on the stream has completed on this
-// PE, and on every member, when the stream passes it).  barrier_kind 0: team_sync_kernel, one
-// workgroup polling the flag row (kPhaseSync, 0) with a bounded spin (*ret on timeout).
-// barrier_kind 1 (ISHMEM_BARRIER_KIND=stream): stream memory operations —
-// hipStreamWriteValue32 of the team's next epoch into this PE's slot of row (kPhaseSync, 1) on
-// every peer (IPC-mapped flag blocks), then hipStreamWaitValue32 (>=) on the p - 1 peer slots of
-// its own row: the command processor waits, no workgroup is resident.  It has no timeout (a
-// missing member stalls the stream, not a bounded spin).  Measured on one GPU (tools/
-// streamop_probe.hip, two streams of one process): a two-party stream-op barrier 9.6 us against
-// 5.7 us for the barrier kernel; which is cheaper over xGMI between processes is for the node run
-// (the N > 1 bench's xgmi_tuning leg times both).  A captured stream (hipGraph) keeps the kernel
-// barrier: a captured write would replay a stale epoch.  Every PE must take the same kind (agreed
-// at init); PEs that differ in capturing one call would use different rows.
+// PE, and on every member, when the stream passes it): team_sync_kernel, one workgroup polling
+// the flag row (kPhaseSync, 0) with a bounded spin (*ret on timeout).  Round 5 also had a barrier
+// of stream memory operations (ISHMEM_BARRIER_KIND=stream: hipStreamWriteValue32 into the peers'
+// rows, hipStreamWaitValue32 on its own); it lost every measurement (2 PEs 20.7 vs 9.3 us per
+// phased call, 8 co-located PEs 651-687 vs 130-175 us, two-stream probe 9.6 vs 5.7 us per
+// barrier), had no timeout, and had to fall back to this kernel under stream capture — a path
+// choice one PE could make differently from its peers — so round 6 removed it.
 int team_barrier(State &s, int team, const ReduceArgs &a, hipStream_t st)
 {
-    if (s.barrier_kind != 1 || a.p <= 1 || capturing(st)) {
-        HIP_TRY(launch_team_sync(a, st));
-        return 0;
-    }
-    uint32_t e = ++s.sb_epoch[team];
-    if (e == 0) e = s.sb_epoch[team] = 1;  // 2^32 barriers of one team: the flags restart at 0
-    const size_t row = ((size_t) kPhaseSync * kMaxBlocks + 1) * kMaxPes;
-    for (int j = 0; j < a.p; ++j)
-        if (j != a.me) HIP_TRY(hipStreamWriteValue32(st, a.peer_flags[j] + row + a.me, e, 0));
-    for (int j = 0; j < a.p; ++j)
-        if (j != a.me) HIP_TRY(hipStreamWaitValue32(st, a.my_flags + row + j, e, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    (void) s;
+    (void) team;
+    HIP_TRY(launch_team_sync(a, st));
     return 0;
 }
 
@@ -767,10 +890,10 @@ int reduce_ll(State &s, int team, int op, int dt, void *dst, const void *src, si
     memset(&a, 0, sizeof(a));
     a.src = (const char *) src;
     a.dst = (char *) dst;
-    a.my_ring = ll_ring(s.flags, team);
+    a.my_ring = s.tmem[team].ring[s.pe];
     for (int j = 0; j < t.size; ++j) {
         const int gpe = t.start + j * t.stride;
-        a.peer_ring[j] = ll_ring(s.peer_flags[gpe], team);
+        a.peer_ring[j] = s.tmem[team].ring[gpe];
         if (!a.peer_ring[j]) return fail("reduce: PE " + std::to_string(gpe) + " ring not mapped");
     }
     a.err = s.err_dev + team;
@@ -836,46 +959,33 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         a.seg_items = pl.seg_items;
     }
     const bool disjoint = d0 + nb <= s0 || s0 + nb <= d0;
-    // Two members, disjoint buffers, up to oneshot_p2 bytes, 16-B body (or shifted sources):
+    // Two members, disjoint buffers, up to the team's fold bound, 16-B body (or shifted sources):
     // barrier, ONE one-shot grid in which each member folds the whole array from both sources,
     // barrier (round 5, PhaseArgs::whole) — the phased path's shape without the all-gather and its
     // barrier.  Over one link it moves the same B per direction as reduce-scatter + all-gather.
-    // Three or four members (round 5): the same whole-array fold while (p - 1) * B <= oneshot_p2 / 4
-    // (8 MiB of peer reads per member by default: 4 MiB at 3 PEs, 2.67 MiB at 4).  On one GPU it
-    // beat the persistent / phased paths up to 8 MiB at 3 PEs and 4 MiB at 4 (1 / 2 MiB at 4 PEs:
-    // 11.3-12.5 / 11.5-12.6 us against 17.9-18.5 / 25.3-25.4); each member pulls (p - 1) * B over
-    // the links where reduce-scatter + all-gather pulls 2(p - 1) / p * B, hence the tighter bound.
-    const bool fold_size = s.direct_p2 && t.size <= s.direct_max_pes &&
-                           (t.size == 2 ? (long long) nb <= s.oneshot_p2
-                                        : (long long) ((uint64_t) (t.size - 1) * nb) <= s.oneshot_p2 / 4);
-    // In place (source == dest): the same fold into a team-private scratch buffer on this device
-    // (dest's 16-B phase; peers never read it, so it is plain device memory, grown on demand),
-    // the end barrier (every member has read every source), then a local copy into dest.  The
-    // staging region with its events was tried first and lost to the persistent kernel
-    // (profiles/r05/direct_p2/r05zzp_*); set_param "direct_inplace" 0 turns this off.
+    // Three or four members (round 5): the same whole-array fold.  On one GPU it beat the
+    // persistent / phased paths up to 8 MiB at 3 PEs and 4 MiB at 4 (1 / 2 MiB at 4 PEs: 11.3-12.5 /
+    // 11.5-12.6 us against 17.9-18.5 / 25.3-25.4); each member pulls (p - 1) * B over the links
+    // where reduce-scatter + all-gather pulls 2(p - 1) / p * B, hence the tighter bound for teams
+    // across GPUs (path_limits).
+    const PathLimits lim = team_limits(s, t);
+    const bool fold_size = lim.fold > 0 && (long long) nb <= lim.fold;
+    // In place (source == dest): the same fold into the team's private scratch on this device
+    // (dest's 16-B phase; peers never read it, so it is plain device memory, allocated with the
+    // team: no allocation on the call path, the same path captured or not), the end barrier (every
+    // member has read every source), then a local copy into dest.  The staging region with its
+    // events was tried first and lost to the persistent kernel (profiles/r05/direct_p2/r05zzp_*);
+    // set_param "direct_inplace" 0 turns this off.
     char *scratch = nullptr;
     // Only while p * B <= 4 MiB: the copy back costs 2B of HBM and a launch, and the fold's gain
     // over the persistent kernel is gone by 2 MiB at 2 PEs and 1 MiB at 4 (2 PEs 1 MiB 12.8-13.4
     // vs 14.9-15.4 us, 4 MiB 20.6-22.4 vs 18.6-19.5; 4 PEs 512 KiB 14.2-14.7 vs 19.7-21.3;
     // profiles/r05/direct_p2/r05zzs_ab_inplace_scratch.txt).
-    if (fold_size && d0 == s0 && pl.vec && s.direct_inplace && (uint64_t) t.size * nb <= (4u << 20) &&
-        !capturing(st)) {
-        const size_t need = nb + 16;
-        if (s.fold_scratch_bytes[team] < need) {
-            if (s.fold_scratch[team]) (void) hipFree(s.fold_scratch[team]);  // synchronises the device
-            s.fold_scratch[team] = nullptr;
-            s.fold_scratch_bytes[team] = 0;
-            const size_t sz = std::max<size_t>(need, 1u << 20);
-            if (hipMalloc((void **) &s.fold_scratch[team], sz) != hipSuccess) {
-                (void) hipGetLastError();
-                s.fold_scratch[team] = nullptr;
-                // Failing is safer than a different path from the peers' (they time out in the
-                // start barrier and report it).
-                return fail("reduce: in-place fold scratch of " + std::to_string(sz) + " bytes not allocated");
-            }
-            s.fold_scratch_bytes[team] = sz;
-        }
-        if (s.fold_scratch[team]) scratch = s.fold_scratch[team] + (d0 & 15);
+    if (fold_size && d0 == s0 && pl.vec && s.direct_inplace && (uint64_t) t.size * nb <= kInplaceFoldBytes) {
+        const TeamMem &m = s.tmem[team];
+        if (!m.fold_scratch || m.fold_scratch_bytes < nb + 16)  // sized for p * B <= 4 MiB at creation
+            return fail("reduce: the team's in-place fold scratch is missing");
+        scratch = m.fold_scratch + (d0 & 15);
     }
     const bool inplace_fold = scratch != nullptr;
     const bool direct = (fold_size && disjoint && (pl.vec || realign)) || inplace_fold;
@@ -932,7 +1042,7 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         s.phase_recorded = s.phase_recorded || ev;
         return 0;
     }
-    if (t.size == 2 && (long long) nb <= s.oneshot_p2 && disjoint) {
+    if (t.size == 2 && (long long) nb <= lim.oneshot && disjoint) {
         a.oneshot = 1;
         a.items_per_chunk = pl.nitems;
         a.seg_items = seg_items(pl.nitems);
@@ -1270,12 +1380,14 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
         if (staged < 0) staged = in_heap(s, src) ? 0 : 1;
         if (nbytes == 0) {
             if (team_sync_locked(s, team, st, ret)) return 1;
-        } else if (!staged && ll_eligible(s, t, dst, src, nbytes) && 2 * nbytes <= ll_capacity(t.size) &&
-                   classify(s, dst) != Kind::Host) {
+        } else if (!staged && ll_eligible(s, t, dst, src, nbytes) && 2 * nbytes <= ll_capacity(t.size)) {
             // Small payloads (round 5): the granule exchange, every member's bytes stored at their
             // team-order offset (kLLCollect) — no start / done handshakes.  Up to half the ring's
             // capacity: the pull kernel moves (p-1)·B where the granules move 2(p-1)·B, and at
-            // 4 PEs x 256 KiB the two were already within 8 % (profiles/r05/ll_coll/).
+            // 4 PEs x 256 KiB the two were already within 8 % (profiles/r05/ll_coll/).  The kernel
+            // stores dest locally whatever its kind (heap, device, pinned host), so the choice
+            // depends on the byte count and the team only: the same on every member (round 6; it
+            // also required a non-host dest, which one member could pass alone — ADVICE r05).
             if (reduce_ll(s, team, ISHMEMI_OP_OR, ISHMEMI_DT_UINT8, dst, src, nbytes, ret, st, kLLCollect)) return 1;
         } else if (staged) {
             if (order_stream(s, st) || collect_staged(s, team, (char *) dst, (const char *) src, nb, ret, st)) return 1;
@@ -1296,7 +1408,6 @@ int fcollect_impl(int team, void *dst, const void *src, size_t nbytes, int *ret,
 // anything that must match across members is launched (a member that failed alone would leave
 // its peers waiting for launches that never come).  Called without the state lock.
 constexpr uint64_t kAgreeStaged = 1ull << 62, kAgreeFail = 1ull << 63;
-constexpr uint64_t kAgreeDestOffHeap = 1ull << 61;  // broadcast: this member's dest is not in the heap
 bool member_call(const State &s, int team);
 
 // The agreement step of the blocking fcollect / collect / scan / broadcast (staged path, counts,
@@ -1385,14 +1496,14 @@ int scan_impl(int team, int dt, int inclusive, void *dst, const void *src, size_
         if (ipc_max == 0) return fail("scan: staging region too small for this team");
         const uintptr_t d0 = (uintptr_t) dst, s0 = (uintptr_t) src, nb = n * es;
         const bool disjoint = d0 + nb <= s0 || s0 + nb <= d0;
-        if (disjoint && (t.size == 2 || (t.size <= s.direct_max_pes &&
-                                         (long long) ((uint64_t) (t.size - 1) * nb) <= s.oneshot_p2 / 4))) {
+        if (disjoint && (t.size == 2 || (long long) nb <= team_limits(s, t).fold)) {
             // Two members, disjoint buffers: barrier, direct one-shot fold, barrier (no scratch;
             // kernels_coll.hip scan_direct_kernel).  Every member sees the same n and the same
             // symmetric offsets, so all take this path together.  At every size past the granule
             // path since round 5 (it was the phased threshold's): 1 / 2 MiB 8.9-9.3 / 9.0 us
             // against the scratch kernel's 17.8-18.1 / 19.7-20.8 (profiles/r05/scan/).  Three and
-            // four members under the reduce's whole-array bound ((p - 1) * B <= oneshot_p2 / 4).
+            // four members under the reduce's whole-array bound (path_limits; 0 with direct_p2
+            // off, so an A/B of direct_p2 switches reduces and scans together — ADVICE r05).
             if (order_stream(s, st)) return 1;
             ScanArgs a;
             memset(&a, 0, sizeof(a));
@@ -1524,11 +1635,6 @@ int reduce_impl(int team, int op, int dt, void *dst, const void *src, size_t n, 
     return 0;
 }
 
-uint32_t *dev_flags(uint32_t *flags_base)
-{
-    return flags_base ? flags_base + (size_t) kMaxTeams * (kTeamFlagBytes / 4) : nullptr;
-}
-
 // Refresh the device copy of the device-API context (after init and after team changes).
 int sync_device_ctx(State &s)
 {
@@ -1543,7 +1649,7 @@ int sync_device_ctx(State &s)
         c.peer_heap[j] = s.peer_heap[j];
         c.peer_dflags[j] = dev_flags(s.peer_flags[j]);
     }
-    c.my_dflags = dev_flags(s.flags);
+    c.my_dflags = dev_flags(s.flags);  // device-API rows of every slot live in the base block
     c.epochs = s.dev_epochs;
     c.dev_counts = (uint64_t *) (s.count_slots + (size_t) kMaxTeams * 64);
     c.err = s.err_dev + kMaxTeams;
@@ -1572,15 +1678,16 @@ const char *flag_kind_name(int k)
     return k == kFlagsUncached ? "uncached" : k == kFlagsFineGrained ? "fine-grained" : "coarse-grained";
 }
 
-// Allocates (zeroed) a flag block of the first kind >= `kind` that this device can allocate AND
-// export over IPC; the kind used is stored in s.flags_kind.  Returns nonzero if none can.
-int alloc_flags(State &s, int kind, bool exportable, hipIpcMemHandle_t *h)
+// Allocates (zeroed) `bytes` of flag memory of the first kind >= `kind` (exactly `kind` when
+// `exact`) that this device can allocate AND, when `exportable`, export over IPC.  Returns nonzero
+// if none can; *out / *kind_out receive the block and its kind.
+int alloc_flag_mem(State &s, size_t bytes, int kind, bool exact, bool exportable, hipIpcMemHandle_t *h,
+                   uint32_t **out, int *kind_out, const char *what)
 {
-    const size_t bytes = kFlagAllocBytes;
     // Test hook: behave as if uncached / fine-grained VRAM could not be allocated (the refusal of
     // coarse-grained flags across devices is tested with it on a one-GPU box).
-    if (s.test_flags_unavailable) kind = kFlagsCoarse;
-    for (int k = kind; k < kFlagKinds; ++k) {
+    if (s.test_flags_unavailable) kind = std::max<int>(kind, kFlagsCoarse);
+    for (int k = kind; k < (exact ? kind + 1 : (int) kFlagKinds); ++k) {
         uint32_t *f = nullptr;
         hipError_t e = k == kFlagsUncached ? hipExtMallocWithFlags((void **) &f, bytes, hipDeviceMallocUncached)
                        : k == kFlagsFineGrained
@@ -1597,14 +1704,61 @@ int alloc_flags(State &s, int kind, bool exportable, hipIpcMemHandle_t *h)
         }
         if (hipMemset(f, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
             (void) hipFree(f);
-            return fail("init: flag block memset failed");
+            return fail(std::string(what) + ": flag block memset failed");
         }
-        s.flags = f;
-        s.flags_kind = k;
+        *out = f;
+        *kind_out = k;
         return 0;
     }
-    return fail(std::string("init: no flag-block memory kind could be allocated and exported") +
-                (exportable ? ipc_hint() : ""));
+    return fail(std::string(what) + ": no flag-block memory of kind " + flag_kind_name(kind) + (exact ? "" : " or lesser") +
+                " could be allocated" + (exportable ? " and exported" + ipc_hint() : ""));
+}
+
+// The base block (init): the first kind >= `kind` this device can allocate and export.
+int alloc_flags(State &s, int kind, bool exportable, hipIpcMemHandle_t *h)
+{
+    return alloc_flag_mem(s, kBaseAllocBytes, kind, false, exportable, h, &s.flags, &s.flags_kind, "init");
+}
+
+// In-place fold scratch of a team of `p` members (reduce_heap): allocated with the team.
+int alloc_fold_scratch(State &s, int team, int p)
+{
+    TeamMem &m = s.tmem[team];
+    if (p < 2) return 0;
+    const size_t bytes = (size_t) (kInplaceFoldBytes / (uint64_t) p) + 256;
+    if (hipMalloc((void **) &m.fold_scratch, bytes) != hipSuccess) {
+        (void) hipGetLastError();
+        m.fold_scratch = nullptr;
+        return fail("team: in-place fold scratch of " + std::to_string(bytes) + " bytes not allocated");
+    }
+    m.fold_scratch_bytes = bytes;
+    return 0;
+}
+
+// Releases a slot's memory on this PE: the imported blocks of its members, its own block (split
+// teams), its fold scratch.  hipFree waits for the device, so no kernel of this PE still uses them;
+// a peer's mapping of this PE's block keeps that memory alive until the peer closes it.
+void release_team_mem(State &s, int team)
+{
+    TeamMem &m = s.tmem[team];
+    if (m.own || m.fold_scratch) (void) hipDeviceSynchronize();  // this PE's kernels are done with them
+    for (int j = 0; j < kMaxPes; ++j)
+        if (m.imported[j]) (void) hipIpcCloseMemHandle(m.imported[j]);
+    if (m.own) {
+        (void) hipFree(m.own);
+        s.team_block_bytes -= kTeamAllocBytes;
+    }
+    if (m.fold_scratch) (void) hipFree(m.fold_scratch);
+    m = TeamMem{};
+}
+
+// Device identity of every PE as small integers (PEs on one GPU share one), from the PCI bus ids
+// allgathered at init; a team is co-located when all its members share one.
+bool team_colocated(const State &s, const Team &t)
+{
+    for (int j = 1; j < t.size; ++j)
+        if (s.dev_id[t.start + j * t.stride] != s.dev_id[t.start]) return false;
+    return true;
 }
 
 int init_impl(int pe, int npes, int device, const std::string &key)
@@ -1669,24 +1823,52 @@ int init_impl(int pe, int npes, int device, const std::string &key)
 #endif
     const bool ep_uncached = env_ll("ISHMEM_EP_UNCACHED", 0) != 0;
     s.phased_peer_nt = env_ll("ISHMEM_PHASED_PEER_NT", 0) != 0;
-    s.barrier_kind = 0;
-    for (int t = 0; t < kMaxTeams; ++t) s.sb_epoch[t] = 0;
-    if (const char *bk = getenv("ISHMEM_BARRIER_KIND"); bk && *bk) {
-        if (strcasecmp(bk, "stream") == 0) s.barrier_kind = 1;
-        else if (strcasecmp(bk, "kernel") != 0 && g_env_error.empty())
-            g_env_error = std::string("ISHMEM_BARRIER_KIND='") + bk + "' is not 'kernel' or 'stream'";
+    // ISHMEM_TEAMS_MAX (src/ishmem/env_defs.h:34, default 64): the team table's size.  Below the 3
+    // predefined teams it is raised to 3, as the reference does (src/teams.cpp:118-119); above 64
+    // init fails as the reference's does (src/teams.cpp:245-248: its slot mask has 64 bits).
+    s.teams_max = kTeamsMaxDefault;
+    if (const char *tm = getenv("ISHMEM_TEAMS_MAX"); tm && *tm) {
+        const long long v = env_ll("ISHMEM_TEAMS_MAX", kTeamsMaxDefault);
+        if (v < 0 && g_env_error.empty())
+            g_env_error = std::string("ISHMEM_TEAMS_MAX='") + tm + "' is not a team count";
+        else if (v > kMaxTeams && g_env_error.empty())
+            g_env_error = "ISHMEM_TEAMS_MAX=" + std::to_string(v) + ": requested " + std::to_string(v) +
+                          " teams, but only " + std::to_string(kMaxTeams) + " are supported";
+        s.teams_max = (int) std::min<long long>(kMaxTeams, std::max<long long>(kPredefTeams, v));
     }
+    // Cross-device teams' thresholds (path_limits): -1 / unset = the link-byte model.
+    s.xgmi_ll_max = std::max<long long>(-1, env_bytes("ISHMEM_XGMI_LL_MAX_BYTES", -1));
+    s.xgmi_fold_max = std::max<long long>(-1, env_bytes("ISHMEM_XGMI_FOLD_MAX_BYTES", -1));
+    s.xgmi_link_bps = 76.8e9;
+    // Round 5's stream-memory-op barrier was removed in round 6 (team_barrier): "kernel" is still
+    // accepted, "stream" is refused rather than silently ignored.
+    if (const char *bk = getenv("ISHMEM_BARRIER_KIND"); bk && *bk && strcasecmp(bk, "kernel") != 0 && g_env_error.empty())
+        g_env_error = std::string("ISHMEM_BARRIER_KIND='") + bk +
+                      "' is not supported: team barriers are the one-workgroup barrier kernel ('kernel')";
     if (!g_env_error.empty()) {
         const std::string e = g_env_error;
         g_env_error.clear();
         return fail("init: " + e);
     }
+    warn_unknown_env();
+
+    using clk = std::chrono::steady_clock;
+    const auto t_start = clk::now();
+    auto t_mark = t_start;
+    auto phase_done = [&](int k) {
+        const auto now = clk::now();
+        s.init_us[k] = std::chrono::duration<double, std::micro>(now - t_mark).count();
+        t_mark = now;
+    };
+    for (double &u : s.init_us) u = 0;
 
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (ndev < 1) return fail("init: no HIP device visible");
     s.device = device >= 0 ? device % ndev : 0;
     HIP_TRY(hipSetDevice(s.device));
+    HIP_TRY(hipFree(nullptr));  // the HIP runtime's own initialisation, timed on its own
+    phase_done(0);
 
     // Symmetric heap: ONE hipMalloc (coarse-grained HBM) per PE, src/memory.cpp:35-132.
     s.heap_size = heap_request;
@@ -1695,6 +1877,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     s.free_list.clear();
     s.used.clear();
     s.free_list[0] = s.heap_size;
+    phase_done(1);
 
     // Barrier flags (written by peers over xGMI): the best memory kind that can also be exported.
     hipIpcMemHandle_t flags_handle{};
@@ -1715,6 +1898,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     }
     s.peer_heap[pe] = s.heap;
     s.peer_flags[pe] = s.flags;
+    for (int i = 0; i < kMaxPes; ++i) s.dev_id[i] = 0;
+    phase_done(2);
 
     if (npes > 1) {
         // Let peers import our dma-buf handles (pidfd_getfd needs ptrace rights under Yama), for
@@ -1739,7 +1924,8 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.phased_min = s.phased_min;
         mine.staging_bytes = s.staging_bytes;
         mine.staging_slots = s.staging_slots;
-        mine.barrier_kind = s.barrier_kind;
+        mine.xgmi_ll_max = s.xgmi_ll_max;
+        mine.xgmi_fold_max = s.xgmi_fold_max;
         if (hipDeviceGetPCIBusId(mine.pci_bus, sizeof(mine.pci_bus), s.device) != hipSuccess) {
             (void) hipGetLastError();
             snprintf(mine.pci_bus, sizeof(mine.pci_bus), "dev%d", s.device);
@@ -1755,6 +1941,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
         mine.flags_handle = flags_handle;
         PeRecord all[kMaxPes];
         if (s.boot.allgather(&mine, all, sizeof(PeRecord), err)) return fail(err);
+        phase_done(3);
         // Agree on the parameters that choose a call's kernel (the minimum over the PEs), so a
         // per-process environment difference cannot split LL from RS/AG or one-shot from RS/AG.
         // The grid cap (max_blocks) stays per PE: the kernels grab work, nothing is paired.
@@ -1764,10 +1951,26 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             s.phased_min = std::max<long long>(s.phased_min, all[j].phased_min);
             s.staging_bytes = std::min<size_t>(s.staging_bytes, all[j].staging_bytes);
             s.staging_slots = (int) std::min<int64_t>(s.staging_slots, all[j].staging_slots);
+            // The cross-device overrides: the smallest value any PE set (-1, the model, only when
+            // none did).
+            if (all[j].xgmi_ll_max >= 0)
+                s.xgmi_ll_max = s.xgmi_ll_max < 0 ? all[j].xgmi_ll_max : std::min<long long>(s.xgmi_ll_max, all[j].xgmi_ll_max);
+            if (all[j].xgmi_fold_max >= 0)
+                s.xgmi_fold_max = s.xgmi_fold_max < 0 ? all[j].xgmi_fold_max
+                                                       : std::min<long long>(s.xgmi_fold_max, all[j].xgmi_fold_max);
         }
         int share = 0;
         for (int j = 0; j < npes; ++j)
             share += strncmp(all[j].pci_bus, mine.pci_bus, sizeof(mine.pci_bus)) == 0;
+        // Device ids: the first PE with the same PCI bus id (identical on every PE).
+        for (int j = 0; j < npes; ++j) {
+            s.dev_id[j] = j;
+            for (int k = 0; k < j; ++k)
+                if (strncmp(all[j].pci_bus, all[k].pci_bus, sizeof(all[j].pci_bus)) == 0) {
+                    s.dev_id[j] = s.dev_id[k];
+                    break;
+                }
+        }
         bool coarse_forced = false;  // a test asked for coarse-grained flags (ISHMEM_FLAGS_KIND=2)
         for (int j = 0; j < npes; ++j) coarse_forced = coarse_forced || all[j].flags_kind_requested == kFlagsCoarse;
         set_device_share(share);
@@ -1775,8 +1978,6 @@ int init_impl(int pe, int npes, int device, const std::string &key)
             if (j == pe) continue;
             if (all[j].heap_size != s.heap_size)
                 return fail("init: ISHMEM_SYMMETRIC_SIZE differs between PEs");
-            if (all[j].barrier_kind != s.barrier_kind)
-                return fail("init: ISHMEM_BARRIER_KIND differs between PEs (the barrier kinds use different flag rows)");
             if (all[j].device != s.device) {
                 // The kernels load peers' memory directly over xGMI: without peer access those
                 // loads would fault the GPU, so refuse to initialise instead.
@@ -1796,6 +1997,7 @@ int init_impl(int pe, int npes, int device, const std::string &key)
                 return fail("init: hipIpcOpenMemHandle of PE " + std::to_string(j) + "'s heap: " + hipGetErrorString(e) +
                             ipc_hint());
         }
+        phase_done(4);
         // Flags (+ LL rings): every PE uses the same memory kind, the least capable one any PE
         // could allocate and export; if some PE cannot import a peer's block of that kind, all
         // step down one kind together and exchange new blocks.
@@ -1861,22 +2063,34 @@ int init_impl(int pe, int npes, int device, const std::string &key)
                         "device's polls.  ISHMEM_FLAGS_KIND=2 forces it anyway (tests only)");
         }
         if (s.boot.barrier(err)) return fail(err);  // every peer has imported our handles
+        phase_done(5);
     }
 
-    // Teams: WORLD, SHARED, NODE all span the node (src/teams.cpp:108-257).
-    for (int i = 0; i < kMaxTeams; ++i) s.teams[i] = Team{};
-    for (int i = 0; i <= ISHMEMI_C_TEAM_NODE; ++i) {
+    // Teams: WORLD, SHARED, NODE all span the node (src/teams.cpp:108-257); their flag blocks and
+    // rings live in the base block of every PE.
+    for (int i = 0; i < kMaxTeams; ++i) {
+        s.teams[i] = Team{};
+        s.tmem[i] = TeamMem{};
+    }
+    s.team_block_bytes = 0;
+    for (int i = 0; i < kPredefTeams; ++i) {
         Team &t = s.teams[i];
         t.valid = true;
         t.start = 0;
         t.stride = 1;
         t.size = npes;
         t.my_idx = pe;
+        t.colocated = team_colocated(s, t);
+        for (int j = 0; j < npes; ++j) {
+            s.tmem[i].flags[j] = base_team_flags(s.peer_flags[j], i);
+            s.tmem[i].ring[j] = base_team_ring(s.peer_flags[j], i);
+        }
+        if (alloc_fold_scratch(s, i, npes)) return 1;
     }
     // Symmetric staging region (first allocation on every PE, hence the same offset).
     s.staging = (char *) heap_alloc(s, s.staging_bytes, kHeapAlign);
     if (!s.staging) return 1;
-    s.team_scratch = (char *) heap_alloc(s, kHeapAlign, kHeapAlign);
+    s.team_scratch = (char *) heap_alloc(s, kTeamScratchBytes, kHeapAlign);
     if (!s.team_scratch) return 1;
     // [0, kMaxTeams) lines: collect_on_stream; [kMaxTeams, 2 kMaxTeams): the device API's collect.
     s.count_slots = (char *) heap_alloc(s, (size_t) 2 * kMaxTeams * 64, kHeapAlign);
@@ -1895,6 +2109,19 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     HIP_TRY(hipMalloc((void **) &s.dev_epochs, kMaxTeams * sizeof(uint32_t)));
     HIP_TRY(hipMemset(s.dev_epochs, 0, kMaxTeams * sizeof(uint32_t)));
     if (sync_device_ctx(s)) return 1;
+    HIP_TRY(hipDeviceSynchronize());
+    phase_done(6);
+    s.init_us[7] = std::chrono::duration<double, std::micro>(clk::now() - t_start).count();
+    if (s.debug > 1) {
+        std::string line;
+        char buf[64];
+        for (int k = 0; k < 8; ++k) {
+            snprintf(buf, sizeof(buf), " %s %.1f", kInitPhase[k], s.init_us[k] / 1000.0);
+            line += buf;
+        }
+        fprintf(stderr, "[ishmem_amd] PE %d init phases (ms):%s (heap %zu MiB, flag block %zu KiB)\n", pe, line.c_str(),
+                s.heap_size >> 20, kBaseAllocBytes >> 10);
+    }
     s.initialized = true;
     write_ctx_slots(s.dctx);
     return 0;
@@ -2163,9 +2390,8 @@ int ishmemi_c_finalize(void)
     (void) hipHostFree(s.err_host);
     (void) hipFree(s.dctx);
     for (int t = 0; t < kMaxTeams; ++t) {
-        if (s.fold_scratch[t]) (void) hipFree(s.fold_scratch[t]);
-        s.fold_scratch[t] = nullptr;
-        s.fold_scratch_bytes[t] = 0;
+        release_team_mem(s, t);
+        s.teams[t] = Team{};
     }
     (void) hipFree(s.dev_epochs);
     (void) hipFree(s.kern_ep);
@@ -2347,9 +2573,11 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
         t.size = size;
         const int d = s.pe - gstart;
         t.my_idx = (d % gstride == 0 && d / gstride >= 0 && d / gstride < size) ? d / gstride : -1;
-        for (int i = ISHMEMI_C_TEAM_NODE + 1; i < kMaxTeams; ++i)
+        t.colocated = team_colocated(s, t);
+        for (int i = kPredefTeams; i < s.teams_max; ++i)
             if (!s.teams[i].valid) free_mask |= 1ull << i;
     }
+    const Team pt = s.teams[parent];
     // Agree on a slot free on every parent member: AND-reduce the free masks over the parent
     // team with the library's own reduction (the reference's bit reduction, teams.cpp:327-345).
     if (hipMemcpy(s.team_scratch, &free_mask, 8, hipMemcpyHostToDevice) != hipSuccess)
@@ -2358,23 +2586,125 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
         return 1;
     if (hipMemcpy(&free_mask, s.team_scratch, 8, hipMemcpyDeviceToHost) != hipSuccess)
         return fail("team_split_strided: mask copy failed");
-    if (!free_mask) return fail("team_split_strided: no team slot free on every parent member");
+    if (!free_mask)  // the same outcome on every parent member (src/teams.cpp:369-371)
+        return fail("team_split_strided: no more teams available (max = " + std::to_string(s.teams_max) +
+                    "), try increasing ISHMEM_TEAMS_MAX");
     const int slot = __builtin_ctzll(free_mask);
+    // The new team's flag block and ring (round 6: per team, not reserved at init).  Every member
+    // allocates one of the kind agreed at init and exports it; the parent exchanges the handles
+    // (an fcollect of one record per parent member through the symmetric team scratch: members
+    // outside the new team send an empty record); each member opens its co-members' blocks.  Both
+    // outcomes are agreed over the parent (AND-reduce), so a failure on one member fails the split
+    // on all of them, with nothing left allocated.  The dma-buf import needs the exporter's ptrace
+    // consent (pidfd_getfd under Yama), given for the exchange only, as at init.
+    struct PtracerWindow {
+        PtracerWindow() { prctl(PR_SET_PTRACER, PR_SET_PTRACER_ANY, 0, 0, 0); }
+        ~PtracerWindow() { prctl(PR_SET_PTRACER, 0, 0, 0, 0); }
+    } ptracer_window;
+    struct SplitRec {
+        uint32_t ok, kind;
+        uint64_t bytes;
+        hipIpcMemHandle_t handle;
+    };
+    static_assert(sizeof(SplitRec) <= kSplitRecBytes && kSplitRecBytes * kMaxPes + 256 <= kTeamScratchBytes,
+                  "split exchange layout");
+    const bool needs_mem = t.my_idx >= 0 && t.size > 1;
+    uint32_t *block = nullptr;
+    SplitRec mine{};
+    std::string why;
+    auto agree = [&](bool ok_here) -> int {  // AND over the parent; -1 if the reduce itself failed
+        uint64_t v = ok_here ? 1 : 0;
+        if (hipMemcpy(s.team_scratch, &v, 8, hipMemcpyHostToDevice) != hipSuccess) return -1;
+        if (ishmemi_c_reduce(parent, ISHMEMI_OP_AND, ISHMEMI_DT_UINT64, s.team_scratch, s.team_scratch, 1)) return -1;
+        if (hipMemcpy(&v, s.team_scratch, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        return v ? 1 : 0;
+    };
+    bool ok = true;
+    if (needs_mem) {
+        std::lock_guard<std::mutex> lk(s.mu);
+        int kind = -1;
+        if (alloc_flag_mem(s, kTeamAllocBytes, s.flags_kind, true, s.npes > 1, &mine.handle, &block, &kind,
+                           "team_split_strided")) {
+            ok = false;
+            why = g_last_error;
+        } else if (alloc_fold_scratch(s, slot, t.size)) {
+            ok = false;
+            why = g_last_error;
+        } else {
+            mine.ok = 1;
+            mine.kind = (uint32_t) kind;
+            mine.bytes = kTeamAllocBytes;
+        }
+    }
+    auto undo = [&]() {
+        std::lock_guard<std::mutex> lk(s.mu);
+        TeamMem &m = s.tmem[slot];
+        for (int j = 0; j < kMaxPes; ++j)
+            if (m.imported[j]) (void) hipIpcCloseMemHandle(m.imported[j]);
+        if (block) (void) hipFree(block);
+        if (m.fold_scratch) (void) hipFree(m.fold_scratch);
+        m = TeamMem{};
+        block = nullptr;
+    };
+    char *rec_src = s.team_scratch + 64, *rec_dst = s.team_scratch + 256;
+    if (hipMemcpy(rec_src, &mine, sizeof(mine), hipMemcpyHostToDevice) != hipSuccess ||
+        ishmemi_c_fcollect(parent, rec_dst, rec_src, kSplitRecBytes)) {
+        undo();  // a local failure of the exchange itself: the peers time out in it and report it
+        return fail("team_split_strided: handle exchange failed: " + std::string(g_last_error));
+    }
+    std::vector<SplitRec> recs((size_t) pt.size);
+    {
+        std::vector<char> raw((size_t) pt.size * kSplitRecBytes);
+        if (hipMemcpy(raw.data(), rec_dst, raw.size(), hipMemcpyDeviceToHost) != hipSuccess) ok = false;
+        for (int i = 0; i < pt.size; ++i) memcpy(&recs[(size_t) i], raw.data() + (size_t) i * kSplitRecBytes, sizeof(SplitRec));
+    }
+    if (needs_mem && ok) {
+        std::lock_guard<std::mutex> lk(s.mu);
+        TeamMem &m = s.tmem[slot];
+        for (int j = 0; j < t.size && ok; ++j) {
+            const int gpe = t.start + j * t.stride;
+            const SplitRec &r = recs[(size_t) ((gpe - pt.start) / pt.stride)];
+            if (!r.ok || r.kind != (uint32_t) s.flags_kind || r.bytes != kTeamAllocBytes) {
+                ok = false;
+                why = "member " + std::to_string(gpe) + " could not allocate its team block";
+                break;
+            }
+            void *p = block;
+            if (gpe != s.pe) {
+                if (hipIpcOpenMemHandle(&p, r.handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                    (void) hipGetLastError();
+                    ok = false;
+                    why = "hipIpcOpenMemHandle of member " + std::to_string(gpe) + "'s team block failed" + ipc_hint();
+                    break;
+                }
+                m.imported[gpe] = p;
+            }
+            m.flags[gpe] = (uint32_t *) p;
+            m.ring[gpe] = (uint64_t *) ((char *) p + kTeamLLOffset);
+        }
+    }
+    const int agreed = agree(ok);
+    if (agreed != 1) {
+        undo();
+        return fail("team_split_strided: the new team's flag blocks could not be set up on every member" +
+                    (why.empty() ? std::string() : " (" + why + ")"));
+    }
     {
         std::lock_guard<std::mutex> lk(s.mu);
         // Only members hold the slot.  A later team that reuses it on a non-member is disjoint
         // from this team (every member of this one has the slot reserved, so the AND-reduced
-        // mask of any parent containing one of them excludes it): flag blocks never collide.
-        if (t.my_idx >= 0) s.teams[slot] = t;
-        s.sb_epoch[slot] = 0;
-        // Fresh flag block: zero it locally, then the parent sync below orders the zeroing
-        // before any member's first barrier on the new team.
-        if (hipMemset(team_flags(s.flags, slot), 0, kTeamFlagBytes) != hipSuccess ||
-            hipMemset(dev_flags(s.flags) + (size_t) slot * kDevFlagWordsPerTeam, 0,
-                      kDevFlagWordsPerTeam * 4) != hipSuccess ||
+        // mask of any parent containing one of them excludes it).
+        if (t.my_idx >= 0) {
+            s.teams[slot] = t;
+            s.tmem[slot].own = block;
+            if (block) s.team_block_bytes += kTeamAllocBytes;
+        }
+        // Launch words and device-API rows of the slot: zero them locally, then the parent sync
+        // below orders the zeroing before any member's first collective on the new team (the
+        // block itself was zeroed before it was exported).
+        if (hipMemset(dev_flags(s.flags) + (size_t) slot * kDevFlagWordsPerTeam, 0, kDevFlagWordsPerTeam * 4) != hipSuccess ||
             hipMemset(s.dev_epochs + slot, 0, sizeof(uint32_t)) != hipSuccess ||
-            hipMemset(s.kern_ep + (size_t) kEpTeamWords * slot, 0, kEpTeamWords * sizeof(uint32_t)) != hipSuccess ||
-            hipMemset(ll_ring(s.flags, slot), 0, kLLTeamBytes) != hipSuccess)
+            hipMemset(s.kern_ep + (size_t) kEpTeamWords * slot, 0, kEpTeamWords * sizeof(uint32_t)) != hipSuccess)
             return fail("team_split_strided: flag reset failed");
         if (sync_device_ctx(s)) return 1;
         if (hipDeviceSynchronize() != hipSuccess) return fail("team_split_strided: sync failed");
@@ -2445,8 +2775,15 @@ void ishmemi_c_team_destroy(int team)
     State &s = S();
     std::lock_guard<std::mutex> lk(s.mu);
     if (team <= ISHMEMI_C_TEAM_NODE || team >= kMaxTeams) return;
-    s.teams[team] = Team{};
-    sync_device_ctx(s);
+    // Local, as in the reference (src/teams.cpp:259-275): the slot is free again on this PE, and
+    // the team's memory goes with it — the co-members' blocks mapped here are closed and this PE's
+    // own block freed (after this PE's kernels are done with it; a co-member that still maps it
+    // keeps the memory alive until it destroys the team too).
+    if (s.initialized) {
+        s.teams[team] = Team{};
+        release_team_mem(s, team);
+        sync_device_ctx(s);
+    }
 }
 
 int ishmemi_c_team_sync(int team)
@@ -2496,15 +2833,13 @@ int ishmemi_c_resync(void)
     if (!s.initialized) return fail("resync: not initialized");
     HIP_TRY(hipDeviceSynchronize());
     struct Epochs {
-        uint32_t host[kMaxTeams], dev[kMaxTeams], sb[kMaxTeams];  // sb: stream barriers (team_barrier)
+        uint32_t host[kMaxTeams], dev[kMaxTeams];
     } mine{}, all[kMaxPes];
+    static_assert(sizeof(Epochs) <= ShmBootstrap::kSlotBytes, "resync exchange");
     std::vector<uint32_t> words((size_t) kMaxTeams * kEpTeamWords);
     HIP_TRY(hipMemcpy(words.data(), s.kern_ep, words.size() * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(mine.dev, s.dev_epochs, sizeof(mine.dev), hipMemcpyDeviceToHost));
-    for (int t = 0; t < kMaxTeams; ++t) {
-        mine.host[t] = words[(size_t) t * kEpTeamWords + kEpEpoch];
-        mine.sb[t] = s.sb_epoch[t];
-    }
+    for (int t = 0; t < kMaxTeams; ++t) mine.host[t] = words[(size_t) t * kEpTeamWords + kEpEpoch];
     if (s.npes > 1) {
         std::string err;
         if (s.boot.allgather(&mine, all, sizeof(Epochs), err)) return fail("resync: " + err);
@@ -2513,13 +2848,11 @@ int ishmemi_c_resync(void)
     }
     auto newest = [](uint32_t a, uint32_t b) { return (int32_t) (b - a) > 0 ? b : a; };
     for (int t = 0; t < kMaxTeams; ++t) {
-        uint32_t h = all[0].host[t], d = all[0].dev[t], sb = all[0].sb[t];
+        uint32_t h = all[0].host[t], d = all[0].dev[t];
         for (int j = 1; j < s.npes; ++j) {
             h = newest(h, all[j].host[t]);
             d = newest(d, all[j].dev[t]);
-            sb = newest(sb, all[j].sb[t]);
         }
-        s.sb_epoch[t] = sb;
         uint32_t *w = words.data() + (size_t) t * kEpTeamWords;
         for (int k = 0; k < kEpTeamWords; ++k) w[k] = 0;
         w[kEpEpoch] = h;
@@ -2764,10 +3097,11 @@ int ishmemi_c_broadcast_on_stream(int team, void *dest, const void *source, size
     if (nbytes == 0) return team_sync_locked(s, team, st, ret) || mark_stream(s, st);
     if (!in_heap(s, source)) return fail("broadcast_on_stream: source must be symmetric-heap memory");
     if (!device_writable(s, dest)) return fail("broadcast_on_stream: dest must be heap, device or pinned host memory");
-    if (in_heap(s, dest) && ll_eligible(s, t, dest, source, nbytes) && 2 * nbytes <= ll_capacity(t.size)) {
+    if (ll_eligible(s, t, dest, source, nbytes) && 2 * nbytes <= ll_capacity(t.size)) {
         // Small payloads (round 5): the root's bytes as granules into every member's ring, the
-        // others one token each (kLLBroadcast) — no handshakes.  Symmetric dest: every member
-        // decides alike.
+        // others one token each (kLLBroadcast) — no handshakes.  Dest is stored locally whatever
+        // its kind, so every member decides alike from the byte count (round 6: the choice no
+        // longer depends on this PE's dest being in the heap — ADVICE r05).
         if (reduce_ll(s, team, ISHMEMI_OP_OR, ISHMEMI_DT_UINT8, dest, source, nbytes, ret, st, kLLBroadcast, root)) return 1;
         return mark_stream(s, st);
     }
@@ -2800,7 +3134,6 @@ int ishmemi_c_broadcast(int team, void *dest, const void *source, size_t nbytes,
     uint64_t mine = 0;
     if (me_root) mine = in_heap(s, source) ? (uint64_t) ((const char *) source - s.heap) : kAgreeStaged;
     if (nbytes && !device_writable(s, dest)) mine |= kAgreeFail;
-    if (!in_heap(s, dest)) mine |= kAgreeDestOffHeap;
     uint64_t all[kMaxPes], any = 0;
     if (team_exchange(team, mine, all)) return 1;
     for (int j = 0; j < p; ++j) any |= all[j];
@@ -2809,10 +3142,10 @@ int ishmemi_c_broadcast(int team, void *dest, const void *source, size_t nbytes,
     uint64_t counts[kMaxPes] = {}, zero[kMaxPes] = {};
     counts[root] = nbytes;
     std::lock_guard<std::mutex> lk(s.mu);
-    if (!(all[root] & kAgreeStaged) && !(any & kAgreeDestOffHeap) && ll_eligible(s, t, dest, source, nbytes) &&
-        2 * nbytes <= ll_capacity(p)) {
-        // Small payloads, every dest in the heap (agreed above): the granule broadcast
-        // (kLLBroadcast); the root reads its own source, the others none.
+    if (!(all[root] & kAgreeStaged) && ll_eligible(s, t, dest, source, nbytes) && 2 * nbytes <= ll_capacity(p)) {
+        // Small payloads, the root's source in the heap (agreed above): the granule broadcast
+        // (kLLBroadcast); the root reads its own source, the others none, and every member
+        // stores its own dest, of any device-writable kind.
         if (reduce_ll(s, team, ISHMEMI_OP_OR, ISHMEMI_DT_UINT8, dest, source, nbytes, nullptr, 0, kLLBroadcast, root))
             return 1;
     } else if (all[root] & kAgreeStaged) {
@@ -2821,7 +3154,7 @@ int ishmemi_c_broadcast(int team, void *dest, const void *source, size_t nbytes,
     } else {
         const char *srcs[kMaxPes];
         const int groot = t.start + root * t.stride;
-        for (int j = 0; j < p; ++j) srcs[j] = s.peer_heap[groot] + (all[root] & ~kAgreeDestOffHeap);
+        for (int j = 0; j < p; ++j) srcs[j] = s.peer_heap[groot] + all[root];
         if (collect_launch(s, team, dest, nullptr, counts, nullptr, 0, zero, srcs)) return 1;
     }
     if (mark_stream(s, 0)) return 1;
@@ -2873,7 +3206,12 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "ll_max_bytes") s.ll_max_bytes = std::min<long long>((long long) kLLMaxBytes, std::max<long long>(0, value));
     else if (n == "debug") s.debug = (int) value;
     else if (n == "phased_peer_nt") s.phased_peer_nt = value != 0;
-    else if (n == "barrier_kind") s.barrier_kind = value != 0 ? 1 : 0;  // measurement: set alike on every PE
+    else if (n == "xgmi_ll_max_bytes") s.xgmi_ll_max = std::max<long long>(-1, value);      // alike on every PE
+    else if (n == "xgmi_fold_max_bytes") s.xgmi_fold_max = std::max<long long>(-1, value);  // alike on every PE
+    else if (n == "xgmi_link_mbps") {
+        if (value <= 0) return fail("set_param: xgmi_link_mbps must be positive");
+        s.xgmi_link_bps = (double) value * 1e6;  // alike on every PE (the model's thresholds follow)
+    }
     else if (n == "realign_grid_cap") set_realign_grid_cap((int) std::min<long long>(std::max<long long>(value, 0), 1 << 30));
     else if (n == "collect_realign") set_collect_realign((int) (value != 0));
     else if (n == "ar_shifted") s.ar_shifted = value != 0;  // measurement: set alike on every PE
@@ -2882,22 +3220,6 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "block_spin") s.block_spin = (int) std::min<long long>(std::max<long long>(value, 0), 2);
     else if (n == "direct_max_pes") s.direct_max_pes = (int) std::min<long long>(std::max<long long>(value, 2), kMaxPes);
     else if (n == "phase_unaligned") set_phase_unaligned((int) (value != 0));
-    else if (n == "stream_barrier_release") {
-        // Escape hatch of the stream barrier, which has no timeout (team_barrier): store the team's
-        // latest stream-barrier epoch into every slot of this PE's own wait row, so a stream stuck
-        // in hipStreamWaitValue32 for a member that never wrote moves on.  For a caller that saw
-        // a stream barrier not complete (bench.py's probe); the barrier's result is then void.
-        const int team = (int) value;
-        if (team < 0 || team >= kMaxTeams || !s.teams[team].valid) return fail("set_param: stream_barrier_release: invalid team");
-        const size_t row = ((size_t) kPhaseSync * kMaxBlocks + 1) * kMaxPes;
-        hipStream_t rs = nullptr;
-        HIP_TRY(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking));
-        hipError_t e = hipMemsetD32Async((hipDeviceptr_t) (team_flags(s.flags, team) + row), (int) s.sb_epoch[team],
-                                         kMaxPes, rs);
-        if (e == hipSuccess) e = hipStreamSynchronize(rs);
-        (void) hipStreamDestroy(rs);
-        if (e != hipSuccess) return hipfail("stream_barrier_release", e);
-    }
     else if (n == "trace_buffer") s.trace = (uint64_t *) (uintptr_t) value;
     else if (n == "phase_events") {
         if (value && !s.phase_ev[0])
@@ -2921,10 +3243,22 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "phased_min_bytes") return s.phased_min == kPhasedOff ? -1 : s.phased_min;
     if (n == "ll_max_bytes") return s.ll_max_bytes;
     if (n == "ll_capacity_bytes") return (long long) ll_capacity(s.npes);  // TEAM_WORLD's ring capacity
-    if (n == "ll_limit_bytes") return (long long) ll_limit(s, s.npes);     // TEAM_WORLD's granule threshold
+    // TEAM_WORLD's thresholds (path_limits: by its topology, co-located or across GPUs).
+    if (n == "ll_limit_bytes") return team_limits(s, s.teams[0]).ll;
+    if (n == "fold_limit_bytes") return team_limits(s, s.teams[0]).fold;
+    if (n == "team_colocated") return s.teams[0].colocated ? 1 : 0;
+    if (n == "xgmi_ll_max_bytes") return s.xgmi_ll_max;
+    if (n == "xgmi_fold_max_bytes") return s.xgmi_fold_max;
+    if (n == "xgmi_link_mbps") return (long long) (s.xgmi_link_bps / 1e6);
+    if (n == "teams_max") return s.teams_max;
+    // Flag memory this PE holds (base block + the split teams' blocks), against round 5's fixed
+    // 16-slot block ("flag_block_bytes_round5").
+    if (n == "flag_block_bytes") return s.initialized ? (long long) (kBaseAllocBytes + s.team_block_bytes) : 0;
+    if (n == "flag_block_bytes_round5") return (long long) kRound5FlagBytes;
+    for (int k = 0; k < 8; ++k)
+        if (n == std::string("init_us_") + kInitPhase[k]) return (long long) s.init_us[k];
     if (n == "debug") return s.debug;
     if (n == "phased_peer_nt") return s.phased_peer_nt;
-    if (n == "barrier_kind") return s.barrier_kind;
     if (n == "realign_grid_cap") return realign_grid_cap();
     if (n == "collect_realign") return collect_realign();
     if (n == "ar_shifted") return s.ar_shifted;
@@ -2977,6 +3311,17 @@ int ishmemi_c_chunk_bounds(uint64_t nitems, int npes, int c, uint64_t *begin, ui
     const uint64_t ipc = npes > 1 ? items_per_chunk(nitems, npes) : nitems;
     *begin = std::min<uint64_t>((uint64_t) c * ipc, nitems);
     *end = std::min<uint64_t>(*begin + ipc, nitems);
+    return 0;
+}
+
+int ishmemi_c_path_limits(int npes, int colocated, long long *ll_limit, long long *fold_limit)
+{
+    if (npes < 1 || npes > kMaxPes || !ll_limit || !fold_limit) return fail("path_limits: invalid arguments");
+    State &s = S();
+    std::lock_guard<std::mutex> lk(s.mu);
+    const PathLimits r = path_limits(s, npes, colocated != 0);
+    *ll_limit = r.ll;
+    *fold_limit = r.fold;
     return 0;
 }
 

@@ -107,46 +107,213 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             # ... and the realigning reduce-scatter kernel (not the default unaligned-load one).
             ish.set_param("phase_unaligned", 0)
 
-        if "sbrelease" in scenarios:
-            # The stream barrier's escape hatch (set_param "stream_barrier_release"): PE 0 enters a
-            # stream-memory-op barrier the others never join; its stream must stay blocked (no
-            # timeout in that barrier), then move on once released; resync agrees the barrier
-            # epochs again and a barrier of every PE completes.
-            import time as _t
-            sst = hip.stream_create()
-            ish.ishmem_barrier_all()
-            ish.set_param("barrier_kind", 1)
-            if pe == 0:
-                if ish.team_sync_on_stream(0, None, sst) != 0:
-                    fails.append(f"pe0 sbrelease: enqueue failed: {ish.last_error()}")
-                _t.sleep(1.0)
-                if hip.stream_query(sst):
-                    fails.append("pe0 sbrelease: a barrier nobody joined completed")
-                if ish.set_param("stream_barrier_release", 0) != 0:
-                    fails.append(f"pe0 sbrelease: release failed: {ish.last_error()}")
-                t0 = _t.monotonic()
-                while not hip.stream_query(sst) and _t.monotonic() - t0 < 10:
-                    _t.sleep(0.01)
-                if not hip.stream_query(sst):
-                    fails.append("pe0 sbrelease: stream still blocked after the release")
-            # PE 0 is one stream barrier ahead: the kernel barrier (its own epochs) lines the PEs up,
-            # then resync agrees the stream-barrier epochs (the maximum).
-            ish.set_param("barrier_kind", 0)
-            ish.ishmem_barrier_all()
-            if ish.resync() != 0:
-                fails.append(f"pe{pe} sbrelease: resync failed: {ish.last_error()}")
-            ish.set_param("barrier_kind", 1)
-            if ish.team_sync_on_stream(0, None, sst) != 0:
-                fails.append(f"pe{pe} sbrelease: barrier after resync failed: {ish.last_error()}")
-            t0 = _t.monotonic()
-            while not hip.stream_query(sst) and _t.monotonic() - t0 < 20:
-                _t.sleep(0.01)
-            if not hip.stream_query(sst):
-                fails.append(f"pe{pe} sbrelease: the all-PE stream barrier after resync did not complete")
-                ish.set_param("stream_barrier_release", 0)
-            hip.stream_synchronize(sst)
-            hip.stream_destroy(sst)
-            ish.set_param("barrier_kind", 0)
+        if "teams61" in scenarios:
+            # ISHMEM_TEAMS_MAX (src/ishmem/env_defs.h:34, src/teams.cpp:118-121,
+            # :369-371): with the default 64 slots a PE holds 61 user teams besides WORLD / SHARED /
+            # NODE.  Each split allocates the team's flag block and ring and exchanges them among its
+            # members (no longer reserved at init), so: the base footprint is at most round 5's fixed
+            # 16-slot block; 61 splits of WORLD succeed, the next fails on every PE naming the
+            # variable; reduces on the last team, a middle one and WORLD (granule and fold sizes,
+            # int32 bit-exact, in place) match the oracle; destroying them all returns the footprint
+            # to the base block, and a second round of splits (slot reuse) works the same.
+            W, INV = ish.ISHMEM_TEAM_WORLD, ish.ISHMEM_TEAM_INVALID
+            tmax = int(ish.get_param("teams_max"))
+            want_max = int(os.environ.get("TEAMS_WANT", 64))
+            fb0, fb5 = int(ish.get_param("flag_block_bytes")), int(ish.get_param("flag_block_bytes_round5"))
+            if tmax != want_max:
+                fails.append(f"pe{pe} teams61: teams_max {tmax} != {want_max}")
+            if not 0 < fb0 <= fb5:
+                fails.append(f"pe{pe} teams61: base flag footprint {fb0} B exceeds round 5's {fb5} B")
+            nmax = 300_000
+            s_t, d_t = heap(nmax, DT["int32"]), heap(nmax, DT["int32"])
+            for rnd in range(2):
+                teams = []
+                for k in range(tmax - 3):
+                    r, t = ish.ishmem_team_split_strided(W, 0, 1, npes)
+                    if r or t == INV:
+                        fails.append(f"pe{pe} teams61 round {rnd}: split {k} failed: {ish.last_error()}")
+                        break
+                    teams.append(t)
+                if sorted(teams) != list(range(3, tmax)):
+                    fails.append(f"pe{pe} teams61 round {rnd}: slots {sorted(teams)[:4]}.. ({len(teams)})")
+                r, t = ish.ishmem_team_split_strided(W, 0, 1, npes)
+                if r == 0 or t != INV or "ISHMEM_TEAMS_MAX" not in ish.last_error():
+                    fails.append(f"pe{pe} teams61 round {rnd}: split past the table: rc={r} team={t} '{ish.last_error()}'")
+                fb = int(ish.get_param("flag_block_bytes"))
+                if teams and (fb <= fb0 or (fb - fb0) % len(teams)):
+                    fails.append(f"pe{pe} teams61: footprint with {len(teams)} teams {fb} B (base {fb0})")
+                for team in ([teams[-1], teams[len(teams) // 2]] if teams else []) + [W]:
+                    for n in (1000, nmax):
+                        ins = [oracle.fill_random(DT["int32"], 6100 + 31 * rnd + 7 * team + j + n, n) for j in range(npes)]
+                        hip.upload(s_t, ins[pe])
+                        if ish.ishmem_int32_sum_reduce(team, d_t, s_t, n):
+                            fails.append(f"pe{pe} teams61 team {team} n={n}: {ish.last_error()}")
+                            continue
+                        check(f"teams61 team {team} n={n}", OPS["sum"], DT["int32"], ins, hip.download(d_t, n, np.int32))
+                        hip.upload(d_t, ins[pe])  # in place
+                        if ish.ishmem_int32_max_reduce(team, d_t, d_t, n):
+                            fails.append(f"pe{pe} teams61 in place team {team} n={n}: {ish.last_error()}")
+                            continue
+                        check(f"teams61 in place team {team} n={n}", OPS["max"], DT["int32"], ins,
+                              hip.download(d_t, n, np.int32))
+                for t in teams:
+                    ish.ishmem_team_destroy(t)
+                if int(ish.get_param("flag_block_bytes")) != fb0:
+                    fails.append(f"pe{pe} teams61: footprint after destroy {ish.get_param('flag_block_bytes')} != {fb0}")
+                ish.ishmem_barrier_all()
+            ish.ishmem_free(d_t)
+            ish.ishmem_free(s_t)
+
+        if "inplacegraph" in scenarios:
+            # the in-place whole-array fold's path no longer depends on stream
+            # capture (its scratch is allocated with the team).  PE 0 captures an in-place f32 sum
+            # into a hipGraph once and replays it; the other PEs call it eagerly, for 1 MiB and
+            # 512 KiB; every result bit-exact against the oracle, each round well within the timeout.
+            gst = hip.stream_create()
+            ret = ish.ishmem_malloc(4)
+            if int(ish.get_param("fold_limit_bytes")) < (1 << 20):
+                fails.append(f"pe{pe} inplacegraph: fold_limit_bytes {ish.get_param('fold_limit_bytes')} < 1 MiB")
+            for nbytes in (1 << 20, 512 << 10):
+                n = nbytes // 4
+                buf = heap(n, DT["float"])
+                ish.ishmem_barrier_all()
+                g = None
+                if pe == 0:
+                    g = hip.Graph(gst)
+                    with g:
+                        if ish.ishmemx_float_sum_reduce_on_stream(buf, buf, n, ret, gst):
+                            fails.append(f"pe0 inplacegraph capture {nbytes}: {ish.last_error()}")
+                for rep in range(4):
+                    vals = [oracle.fill_random(DT["float"], 8800 + 10 * rep + j + n, n) for j in range(npes)]
+                    hip.upload(buf, vals[pe])
+                    hip.memset(ret, 0xFF, 4)
+                    ish.ishmem_barrier_all()
+                    t0 = time.monotonic()
+                    if pe == 0:
+                        g.launch()
+                    elif ish.ishmemx_float_sum_reduce_on_stream(buf, buf, n, ret, gst):
+                        fails.append(f"pe{pe} inplacegraph eager {nbytes}: {ish.last_error()}")
+                    hip.stream_synchronize(gst)
+                    if time.monotonic() - t0 > 5.0:
+                        fails.append(f"pe{pe} inplacegraph {nbytes} rep {rep}: {time.monotonic() - t0:.1f} s")
+                    if int(hip.download(ret, 1, np.int32)[0]) != 0:
+                        fails.append(f"pe{pe} inplacegraph {nbytes} rep {rep}: ret != 0")
+                    check(f"inplacegraph {nbytes} rep {rep}", OPS["sum"], DT["float"], vals, hip.download(buf, n, np.float32))
+                del g
+                ish.ishmem_free(buf)
+            hip.stream_destroy(gst)
+            ish.ishmem_free(ret)
+
+        if "mixeddest" in scenarios:
+            # the granule fcollect / broadcast no longer choose their path from
+            # this PE's dest kind.  PE 0 passes a pinned-host (blocking) or plain device (on a
+            # stream) dest, the others a heap dest; granule and pull sizes; every dest checked.
+            m_small, m_big = 1000, 300_000
+            src_m = ish.ishmem_malloc(4 * m_big)
+            dheap = ish.ishmem_malloc(4 * m_big * npes)
+            ddev = hip.malloc(4 * m_big * npes)
+            hdst = hip.host_malloc(4 * m_big * npes)
+            hv = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_int32 * (m_big * npes)).from_address(hdst))
+            mst = hip.stream_create()
+            ret = ish.ishmem_malloc(4)
+            for m in (m_small, m_big):
+                vals = [oracle.fill_random(DT["int32"], 9100 + j + m, m) for j in range(npes)]
+                hip.upload(src_m, vals[pe])
+                want = np.concatenate(vals)
+                ish.ishmem_barrier_all()
+                dst = hdst if pe == 0 else dheap
+                if ish.ishmem_int32_fcollect(dst, src_m, m):
+                    fails.append(f"pe{pe} mixeddest fcollect m={m}: {ish.last_error()}")
+                else:
+                    got = hv[:m * npes].copy() if pe == 0 else hip.download(dheap, m * npes, np.int32)
+                    if not np.array_equal(got, want):
+                        fails.append(f"pe{pe} mixeddest fcollect m={m} wrong")
+                dst = ddev if pe == 0 else dheap
+                hip.memset(ret, 0xFF, 4)
+                rc = [ish.fcollect_on_stream(dst, src_m, 4 * m, ret, mst)]
+                hip.stream_synchronize(mst)
+                got = hip.download(dst, m * npes, np.int32)
+                if rc[0] or int(hip.download(ret, 1, np.int32)[0]) != 0 or not np.array_equal(got, want):
+                    fails.append(f"pe{pe} mixeddest fcollect_on_stream m={m} rc={rc} {ish.last_error()}")
+                root = npes - 1
+                hip.memset(ret, 0xFF, 4)
+                rc = [ish.broadcast_on_stream(dst, src_m, 4 * m, root, ret, mst)]
+                hip.stream_synchronize(mst)
+                if rc[0] or int(hip.download(ret, 1, np.int32)[0]) != 0 or \
+                        not np.array_equal(hip.download(dst, m, np.int32), vals[root]):
+                    fails.append(f"pe{pe} mixeddest broadcast_on_stream m={m} rc={rc} {ish.last_error()}")
+                dst = hdst if pe == 0 else dheap
+                if ish.ishmem_int32_broadcast(dst, src_m, m, root):
+                    fails.append(f"pe{pe} mixeddest broadcast m={m}: {ish.last_error()}")
+                else:
+                    got = hv[:m].copy() if pe == 0 else hip.download(dheap, m, np.int32)
+                    if not np.array_equal(got, vals[root]):
+                        fails.append(f"pe{pe} mixeddest broadcast m={m} wrong")
+            hip.stream_destroy(mst)
+            del hv
+            hip.host_free(hdst)
+            hip.free(ddev)
+            for b_ in (ret, dheap, src_m):
+                ish.ishmem_free(b_)
+
+        if "hostread" in scenarios:
+            # a blocking call returns on a stream-written host word, without
+            # hipStreamSynchronize (host_wait).  A pinned-host dest is read by the host at once, a
+            # plain device dest copied out at once on another (non-blocking) stream; reduce (granule,
+            # fold / staged sizes) and fcollect, new inputs every round.
+            nmax = 300_000
+            src_h = ish.ishmem_malloc(4 * nmax)
+            ddev = hip.malloc(4 * nmax * npes)
+            hdst = hip.host_malloc(4 * nmax * npes)
+            hout = hip.host_malloc(4 * nmax * npes)
+            hv = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_int32 * (nmax * npes)).from_address(hdst))
+            ho = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_int32 * (nmax * npes)).from_address(hout))
+            nb_st = hip.stream_create()
+            for rnd in range(3):
+                for n in (1000, nmax):
+                    ins = [oracle.fill_random(DT["int32"], 9300 + 17 * rnd + j + n, n) for j in range(npes)]
+                    hip.upload(src_h, ins[pe])
+                    red = oracle.reduce_fold(OPS["sum"], DT["int32"], ins, 0)
+                    ish.ishmem_barrier_all()
+                    hv[:n] = -1
+                    if ish.ishmem_int32_sum_reduce(hdst, src_h, n):
+                        fails.append(f"pe{pe} hostread reduce pinned n={n}: {ish.last_error()}")
+                    elif not np.array_equal(hv[:n], red):
+                        fails.append(f"pe{pe} hostread reduce into pinned host n={n} round {rnd}: not final at return")
+                    if ish.ishmem_int32_sum_reduce(ddev, src_h, n):
+                        fails.append(f"pe{pe} hostread reduce device n={n}: {ish.last_error()}")
+                    else:
+                        hip.memcpy_async(hout, ddev, 4 * n, nb_st)
+                        hip.stream_synchronize(nb_st)
+                        if not np.array_equal(ho[:n], red):
+                            fails.append(f"pe{pe} hostread reduce into device n={n} round {rnd}: not final at return")
+                    hv[:n * npes] = -1
+                    if ish.ishmem_int32_fcollect(hdst, src_h, n):
+                        fails.append(f"pe{pe} hostread fcollect pinned n={n}: {ish.last_error()}")
+                    elif not np.array_equal(hv[:n * npes], np.concatenate(ins)):
+                        fails.append(f"pe{pe} hostread fcollect into pinned host n={n} round {rnd}: not final at return")
+            hip.stream_destroy(nb_st)
+            del hv, ho
+            hip.host_free(hout)
+            hip.host_free(hdst)
+            hip.free(ddev)
+            ish.ishmem_free(src_h)
+
+        if "pathparam" in scenarios:
+            # TEAM_WORLD's thresholds follow its topology — one PE per (emulated)
+            # GPU takes the link-byte model's, co-located PEs round 5's measured ones — and agree
+            # with the library's own path_limits for that shape.
+            import ctypes
+            coloc = int(os.environ.get("COLOCATED_WANT", 1))
+            if int(ish.get_param("team_colocated")) != coloc:
+                fails.append(f"pe{pe} team_colocated {ish.get_param('team_colocated')} != {coloc}")
+            ll, fo = ctypes.c_longlong(), ctypes.c_longlong()
+            ish.lib().ishmemi_c_path_limits(npes, coloc, ctypes.byref(ll), ctypes.byref(fo))
+            if (int(ish.get_param("ll_limit_bytes")), int(ish.get_param("fold_limit_bytes"))) != (ll.value, fo.value):
+                fails.append(f"pe{pe} limits {ish.get_param('ll_limit_bytes')}/{ish.get_param('fold_limit_bytes')} "
+                             f"!= path_limits {ll.value}/{fo.value}")
+            if "LL_LIMIT_WANT" in os.environ and int(ish.get_param("ll_limit_bytes")) != int(os.environ["LL_LIMIT_WANT"]):
+                fails.append(f"pe{pe} ll_limit_bytes {ish.get_param('ll_limit_bytes')} != {os.environ['LL_LIMIT_WANT']}")
 
         if "phaseevents" in scenarios:
             # The measurement hook: a phased reduce with events between its five launches.

@@ -72,15 +72,37 @@ def test_multi_pe_kernel_follows_the_phased_threshold():
     assert k.startswith("rs_phase_kernel")
     assert b.multi_pe_kernel(B, -1).startswith("allreduce_kernel")
     assert b.multi_pe_kernel(64 << 20, 128 << 20).startswith("allreduce_kernel")
-    # Two members up to oneshot_p2: the whole-array fold between two barriers (HBM 3B per PE).
+    # Up to the team's fold bound (get_param "fold_limit_bytes": co-located 2 PEs 32 MiB): the
+    # whole-array fold between two barriers (HBM 3B per PE).
     k2 = b.multi_pe_kernel(16 << 20, 4 << 20, 2, 32 << 20)
     assert "whole-array" in k2 and b.multi_pe_kernel(64 << 20, 4 << 20, 2, 32 << 20).startswith("rs_phase_kernel<float,SUM,P>")
     r2, t2 = b.roofline(2, 2, 16 << 20, 0.02, k2)
     assert "2 x 3 x B" in r2["kernel"] and abs(t2 - 2 * 3 * (16 << 20) / 8e12) < 1e-12
-    # Three / four members while (p - 1) * B <= oneshot_p2 / 4; every member pulls (p - 1) * B.
-    k4 = b.multi_pe_kernel(2 << 20, 4 << 20, 4, 32 << 20)
-    assert "whole-array" in k4 and "whole-array" not in b.multi_pe_kernel(4 << 20, 4 << 20, 4, 32 << 20)
+    # Four members (co-located bound 32 MiB / 4 / 3); every member pulls (p - 1) * B.
+    k4 = b.multi_pe_kernel(2 << 20, 4 << 20, 4, (32 << 20) // 12)
+    assert "whole-array" in k4 and "whole-array" not in b.multi_pe_kernel(4 << 20, 4 << 20, 4, (32 << 20) // 12)
+    assert "whole-array" not in b.multi_pe_kernel(1 << 10, 4 << 20, 8, 0)  # no fold past 4 members
     r4, t4 = b.roofline(4, 1, 2 << 20, 0.02, k4)
     assert "(p-1)*B" in r4["kernel"] and abs(t4 - max(5 * (2 << 20) / 8e12, (2 << 20) / 153.6e9)) < 1e-12
     roof, _ = b.roofline(2, 2, B, 0.84, k)
     assert roof["kernel"].startswith("rs_phase_kernel") and 0 < roof["frac"] <= 1
+
+
+def test_recommended_thresholds_from_the_tuning_rows():
+    # the N > 1 line turns its xgmi_tuning rows into the environment a run on
+    # that topology would set (cross-device variables when one PE per GPU).
+    b = _bench()
+    rows = [{"case": "ll_on", "bytes": 4096, "us": 4.0}, {"case": "ll_off", "bytes": 4096, "us": 9.0},
+            {"case": "ll_on", "bytes": 65536, "us": 6.0}, {"case": "ll_off", "bytes": 65536, "us": 9.5},
+            {"case": "ll_on", "bytes": 262144, "us": 12.0}, {"case": "ll_off", "bytes": 262144, "us": 10.0},
+            {"case": "fold", "bytes": 1 << 20, "us": 9.0}, {"case": "no_fold", "bytes": 1 << 20, "us": 11.0},
+            {"case": "fold", "bytes": 4 << 20, "us": 12.0}, {"case": "no_fold", "bytes": 4 << 20, "us": 13.0},
+            {"case": "p2_oneshot", "bytes": 1 << 30, "us": 800.0}, {"case": "p2_rs_ag", "bytes": 1 << 30, "us": 840.0},
+            {"case": "phased", "bytes": 2 << 20, "us": 15.0}, {"case": "persistent", "bytes": 2 << 20, "us": 14.0},
+            {"case": "phased", "bytes": 4 << 20, "us": 16.0}, {"case": "persistent", "bytes": 4 << 20, "us": 17.0},
+            {"case": "phased", "bytes": 1 << 30, "us": 850.0}, {"case": "persistent", "bytes": 1 << 30, "us": 990.0}]
+    r = b.recommended(rows, 2, 1, 1 << 30)
+    assert r["env"] == {"ISHMEM_XGMI_LL_MAX_BYTES": 65536, "ISHMEM_XGMI_FOLD_MAX_BYTES": 1 << 30,
+                        "ISHMEM_PHASED_MIN_BYTES": 4 << 20}, r
+    r8 = b.recommended([x for x in rows if not x["case"].startswith(("fold", "no_fold", "p2"))], 8, 8, 1 << 30)
+    assert r8["env"] == {"ISHMEM_LL_MAX_BYTES": 65536, "ISHMEM_PHASED_MIN_BYTES": 4 << 20}, r8

@@ -219,21 +219,6 @@ def test_phased_reduce_scatter_allgather_path(npes):
 
 
 @pytest.mark.parametrize("npes", [2, 3, 8])
-def test_phased_path_with_stream_memop_barriers(npes):
-    # ISHMEM_BARRIER_KIND=stream: the phased paths' team barriers (and
-    # ishmem_team_sync) as hipStreamWriteValue32 into the peers' flag rows + hipStreamWaitValue32 on
-    # the own row, instead of the one-workgroup barrier kernel.  Forced for every heap reduce with a
-    # 16-B body: golden inputs, in place, the offset sweeps, edges, 256 MiB in full, hipGraph replay
-    # (captured calls keep the kernel barrier) and the chained-producer tripwire; plus the phased
-    # collect / scan at 2 and 3 PEs.
-    scen = ["golden", "inplace", "offsets", "offsets_large", "edge", "large", "graph", "tripwire"]
-    if npes < 8:
-        scen += ["collect", "scan"]
-    run_pes(npes, scen, env={"ISHMEM_BARRIER_KIND": "stream", "ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0,
-                             "ISHMEM_ONESHOT_P2_MAX_BYTES": 0, "ISHMEM_MAX_BLOCKS": 64}, timeout=400)
-
-
-@pytest.mark.parametrize("npes", [2, 3, 8])
 def test_realigned_reduce_scatter_grid_stride_loop(npes):
     # The phased path forced, sources on other 16-B phases than dest (offsets_large), with the
     # realigned reduce-scatter capped at 3 workgroups: its grid-stride loop, which otherwise runs
@@ -241,13 +226,6 @@ def test_realigned_reduce_scatter_grid_stride_loop(npes):
     run_pes(npes, ["realigncap", "offsets_large"],
             env={"ISHMEM_PHASED_MIN_BYTES": 0, "ISHMEM_LL_MAX_BYTES": 0, "ISHMEM_ONESHOT_P2_MAX_BYTES": 0},
             timeout=300)
-
-
-@pytest.mark.parametrize("npes", [2, 3])
-def test_stream_barrier_release_unblocks_a_barrier_nobody_joined(npes):
-    # The stream barrier has no timeout; bench.py's probe relies on this escape hatch to keep a
-    # barrier that never completes from hanging the measured line.
-    run_pes(npes, ["sbrelease", "golden"], env={"ISHMEM_PHASED_MIN_BYTES": 0}, timeout=180)
 
 
 @pytest.mark.parametrize("npes", [2, 4])
@@ -279,10 +257,48 @@ def test_one_pe_per_gpu_configuration_emulated(npes):
     # PE sized its persistent grid for the whole GPU, and eight such waiting grids on one device
     # timed out in the tripwire (profiles/r03/phased_share/r03zh_*).  Now every waiting launch takes
     # at most 1 / wait_slots of the device (kernels.h, "Waiting footprint"), so eight fit at once.
+    # Round 6: the team spans (emulated) GPUs, so its thresholds come from the link-byte model
+    # (runtime.cpp path_limits; pathparam checks them against the C-ABI's and the restatement in
+    # tests/test_path_limits.py) — the granule threshold differs from the co-located run's.
+    from tests.test_path_limits import expected
     env = {**TESTHOOKS, "ISHMEM_TEST_PCI_BUS": [f"fake-bus-{i}" for i in range(npes)], "ISHMEM_MAX_BLOCKS": 1024,
-           "ISHMEM_PHASED_MIN_BYTES": "", "PHASED_WANT": 4 << 20}
-    run_pes(npes, ["phasedparam", "golden", "inplace", "edge", "large", "graph", "tripwire"], env=env,
+           "ISHMEM_PHASED_MIN_BYTES": "", "PHASED_WANT": 4 << 20, "COLOCATED_WANT": 0,
+           "LL_LIMIT_WANT": expected(npes, False)[0]}
+    run_pes(npes, ["phasedparam", "pathparam", "golden", "inplace", "edge", "large", "graph", "tripwire"], env=env,
             timeout=400)
+
+
+@pytest.mark.parametrize("npes", [2, 4])
+def test_path_thresholds_of_a_colocated_world(npes):
+    # The co-located counterpart of the emulated test above: round 5's measured crossovers.
+    from tests.test_path_limits import expected
+    run_pes(npes, ["pathparam"], env={"COLOCATED_WANT": 1, "LL_LIMIT_WANT": expected(npes, True)[0]}, timeout=120)
+
+
+@pytest.mark.parametrize("npes,teams_max", [(2, None), (4, 8)])
+def test_teams_max_split_allocates_team_memory(npes, teams_max):
+    # ISHMEM_TEAMS_MAX (default 64) sizes the team table; each split allocates
+    # and exchanges the new team's flag block and ring.  2 PEs: 61 user teams, the 62nd refused
+    # naming the variable, reduces on the last / a middle team / WORLD vs the oracle, destroy and
+    # re-split; 4 PEs with ISHMEM_TEAMS_MAX=8: 5 teams.
+    env = {"ISHMEM_TEAMS_MAX": teams_max if teams_max else "", "TEAMS_WANT": teams_max or 64}
+    run_pes(npes, ["teams61", "team"], env=env, timeout=300)
+
+
+@pytest.mark.parametrize("npes", [2, 3, 4])
+def test_inplace_fold_captured_on_one_pe_eager_on_the_others(npes):
+    # PE 0 replays a captured in-place 1 MiB / 512 KiB f32 sum while the others
+    # call it eagerly (granule path off, so both sizes take the in-place fold); then the graph and
+    # in-place scenarios on the same world.
+    run_pes(npes, ["inplacegraph", "inplace", "graph"], env={"ISHMEM_LL_MAX_BYTES": 0}, timeout=240)
+
+
+@pytest.mark.parametrize("npes", [2, 3])
+def test_collectives_with_members_passing_different_dest_kinds(npes):
+    # PE 0's dest pinned host (blocking) or plain device memory (on a stream), the
+    # others' in the heap — the granule fcollect / broadcast decide alike on every member; and the
+    # blocking calls' dest read at once by the host (pinned) or another stream (device memory).
+    run_pes(npes, ["mixeddest", "hostread"], timeout=240)
 
 
 @pytest.mark.parametrize("npes,slots", [(2, 16), (4, 16), (8, 32)])

@@ -29,7 +29,8 @@ LAUNCH_VARS = ("ISHMEM_PE", "ISHMEM_NPES", "ISHMEM_DEVICE", "ISHMEM_BOOTSTRAP_KE
                "SLURM_NPROCS", "SLURM_LOCALID", "SLURM_JOB_ID", "SLURM_STEP_ID", "SLURM_NTASKS_PER_NODE",
                "SLURM_STEP_NUM_TASKS", "SLURM_STEP_NUM_NODES", "ISHMEM_ENABLE_GPU_IPC",
                "ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "ISHMEM_WAIT_SLOTS", "ISHMEM_TEST_PCI_BUS",
-               "ISHMEM_TEST_FLAGS_UNAVAILABLE", "GPU_MAX_HW_QUEUES", "ISHMEM_BARRIER_KIND", "ISHMEM_DEBUG")
+               "ISHMEM_TEST_FLAGS_UNAVAILABLE", "GPU_MAX_HW_QUEUES", "ISHMEM_BARRIER_KIND", "ISHMEM_DEBUG",
+               "ISHMEM_TEAMS_MAX", "ISHMEM_XGMI_LL_MAX_BYTES", "ISHMEM_XGMI_FOLD_MAX_BYTES")
 
 # One process: what ishmemi_c_init would use, then (optionally) the native bootstrap's allgather
 # among the PEs it names.
@@ -195,9 +196,17 @@ print("rc=%d|%s" % (rc, L.ishmemi_c_last_error().decode()))
     ("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "FALSE", False), ("ISHMEM_ENABLE_ACCESSIBLE_HOST_HEAP", "0", False),
     # ISHMEM_DEBUG is the reference's boolean (env_utils.cpp:138-149): "true" / "yes" are valid
     ("ISHMEM_DEBUG", "true", False), ("ISHMEM_DEBUG", "yes", False), ("ISHMEM_DEBUG", "2", False),
-    # the team-barrier kind: kernel (default) or stream memory operations
-    ("ISHMEM_BARRIER_KIND", "stream", False), ("ISHMEM_BARRIER_KIND", "Kernel", False),
+    # the team-barrier kind: the kernel only since round 6 (the stream-memory-op barrier was removed,
+    # DESIGN.md §7); "stream" is refused by name rather than silently ignored
+    ("ISHMEM_BARRIER_KIND", "stream", True), ("ISHMEM_BARRIER_KIND", "Kernel", False),
     ("ISHMEM_BARRIER_KIND", "cp", True),
+    # the team table's size: the reference's variable, default 64, at most 64
+    # (src/ishmem/env_defs.h:34, src/teams.cpp:245-248); below 3 it is raised to 3 (teams.cpp:119)
+    ("ISHMEM_TEAMS_MAX", "abc", True), ("ISHMEM_TEAMS_MAX", "65", True), ("ISHMEM_TEAMS_MAX", "64x", True),
+    ("ISHMEM_TEAMS_MAX", "-1", True), ("ISHMEM_TEAMS_MAX", "64", False), ("ISHMEM_TEAMS_MAX", "1", False),
+    # cross-device thresholds: byte counts, -1 = the link-byte model
+    ("ISHMEM_XGMI_LL_MAX_BYTES", "256K", False), ("ISHMEM_XGMI_LL_MAX_BYTES", "lots", True),
+    ("ISHMEM_XGMI_FOLD_MAX_BYTES", "-1", False), ("ISHMEM_XGMI_FOLD_MAX_BYTES", "8MiBs", True),
     # test hooks exist only in libishmem_amd_testhooks.so
     ("ISHMEM_TEST_PCI_BUS", "fake-bus-0", True), ("ISHMEM_TEST_FLAGS_UNAVAILABLE", "1", True),
     ("ISHMEM_TIMEOUT_MS", "99999999999999999999", True), ("ISHMEM_FLAGS_KIND", "1.5", True),
@@ -254,3 +263,16 @@ def test_library_sets_ipc_mode_when_loaded(preset, want):
                          timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip().splitlines()[-1] == f"value={want}", out.stdout
+
+
+def test_unknown_ishmem_variable_warns_like_the_reference():
+    """The reference warns about an ISHMEM_* name it does not define and carries on
+    (src/env_utils.cpp:193-196); so does ishmemi_c_init.  The reference's own variables that this
+    path has no use for (ISHMEM_NBI_COUNT, ...) are accepted silently."""
+    out = subprocess.run([sys.executable, "-c", ENV_PROBE, str(ROOT)],
+                         env=clean_env(ISHMEM_NO_SUCH_KNOB="1", ISHMEM_NBI_COUNT="8"), capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "Environment variable 'ISHMEM_NO_SUCH_KNOB' is not a supported variable" in out.stderr
+    assert "ISHMEM_NBI_COUNT" not in out.stderr
+    assert "ISHMEM_NO_SUCH_KNOB" not in out.stdout.strip().splitlines()[-1]  # a warning, not an init error
