@@ -249,6 +249,9 @@ struct PhaseArgs {
     // 1: every member folds the WHOLE array (two-member direct path, runtime.cpp reduce_heap): the
     // reduce-scatter grid over all items and both edges, no all-gather.
     int whole;
+    // Shifted sources (shift != 0) on rs_phase_kernel: 1 = XCD-grouped block order (default since
+    // round 6, kernels_impl.h xcd_grouped_block), 0 = block order (set_param "rs_xcd", A/B only).
+    int xcd_group;
 };
 hipError_t launch_rs_phase(int op, int dt, const PhaseArgs &a, hipStream_t s);
 hipError_t launch_ag_phase(const PhaseArgs &a, hipStream_t s);

@@ -1202,6 +1202,21 @@ __device__ __forceinline__ void rs_phase_edges(const PhaseArgs &a)
     }
 }
 
+// XCD-grouped block order (round 6): the hardware hands workgroup b to XCD b mod 8, so in a
+// one-shot grid neighbouring 1 KiB blocks land on different XCDs, whose L2s are separate.  Within
+// each full group of 64 workgroups, XCD x takes logical blocks 8x .. 8x + 7 instead: neighbouring
+// blocks share an L2.  For sources read with unaligned 16-B loads (the shifted reduce-scatter) the
+// line at each block boundary is then fetched once, not by two XCDs: 1 GiB a + b from sources 4 /
+// 12 B off dest's phase, one-wave workgroups, 0.537 / 0.536 ms in block order against 0.484 /
+// 0.483 ms grouped (0.75 -> 0.83 of HBM; tools/realign_variants.hip "unal 64 xcd",
+// profiles/r06/realign/).  A permutation of [0, grid): the tail past the last full group keeps
+// its index.
+__device__ __forceinline__ uint64_t xcd_grouped_block(uint64_t b, uint64_t grid)
+{
+    if (b >= (grid & ~63ull)) return b;
+    return (b & ~63ull) | ((b & 7) << 3) | ((b >> 3) & 7);
+}
+
 template <typename T, int OP, int P>
 __global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
 {
@@ -1210,8 +1225,9 @@ __global__ __launch_bounds__(kFaninBlock) void rs_phase_kernel(PhaseArgs a)
     const uint64_t ce = a.whole ? a.nitems : min(cs + a.items_per_chunk, a.nitems);
     const uint64_t head_bytes = a.head * sizeof(T);
     const uint64_t stride = (uint64_t) gridDim.x * kFaninBlock;
+    const uint64_t blk = a.shift && a.xcd_group ? xcd_grouped_block(blockIdx.x, gridDim.x) : blockIdx.x;
     auto body = [&](auto nt) {
-        for (uint64_t i0 = cs + (uint64_t) blockIdx.x * kFaninBlock; i0 < ce; i0 += stride) {
+        for (uint64_t i0 = cs + blk * kFaninBlock; i0 < ce; i0 += stride) {
             const bool valid = i0 + threadIdx.x < ce;
             const uint64_t wb = head_bytes + i0 * 16;
             if constexpr (P > 0) rs_phase_dispatch<T, OP, P, decltype(nt)::value>(a, (int) ((i0 / kFaninBlock) % P), wb, valid);

@@ -394,6 +394,8 @@ struct State {
     // default 1): vector items laid out by dest, the sources read with unaligned 16-B loads;
     // 0 = the element-granular instantiation (A/B only).
     int ar_shifted = 1;
+    // The shifted reduce-scatter's block order (PhaseArgs::xcd_group; set_param "rs_xcd", default 1).
+    int rs_xcd = 1;
     // Two-member disjoint reduces up to oneshot_p2 bytes: barrier + one whole-array fold grid +
     // barrier (1, default) or the persistent kernel's one-shot mode (0; set_param "direct_p2",
     // alike on every PE).
@@ -1008,6 +1010,7 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         ph.me = t.my_idx;
         ph.peer_nt = s.phased_peer_nt;
         ph.whole = direct ? 1 : 0;
+        ph.xcd_group = s.rs_xcd;
         if (inplace_fold) ph.dst = scratch;
         if (realign) {
             const uint64_t h = std::min<uint64_t>(n, ((16 - d0 % 16) % 16) / es);
@@ -3215,6 +3218,7 @@ int ishmemi_c_set_param(const char *name, long long value)
     else if (n == "realign_grid_cap") set_realign_grid_cap((int) std::min<long long>(std::max<long long>(value, 0), 1 << 30));
     else if (n == "collect_realign") set_collect_realign((int) (value != 0));
     else if (n == "ar_shifted") s.ar_shifted = value != 0;  // measurement: set alike on every PE
+    else if (n == "rs_xcd") s.rs_xcd = value != 0;          // measurement (local: no pairing)
     else if (n == "direct_p2") s.direct_p2 = value != 0;  // measurement: set alike on every PE
     else if (n == "direct_inplace") s.direct_inplace = value != 0;  // measurement: set alike on every PE
     else if (n == "block_spin") s.block_spin = (int) std::min<long long>(std::max<long long>(value, 0), 2);
@@ -3262,6 +3266,7 @@ long long ishmemi_c_get_param(const char *name)
     if (n == "realign_grid_cap") return realign_grid_cap();
     if (n == "collect_realign") return collect_realign();
     if (n == "ar_shifted") return s.ar_shifted;
+    if (n == "rs_xcd") return s.rs_xcd;
     if (n == "direct_p2") return s.direct_p2;
     if (n == "direct_inplace") return s.direct_inplace;
     if (n == "block_spin") return s.block_spin;

@@ -272,6 +272,51 @@ __global__ __launch_bounds__(64) void k_dpp2(Args a)
     if (i0 + 64 + tid < a.nitems) wt(db, tid * 16u + 1024u, acc[1]);
 }
 
+// Round 6: the neighbour within the wave by DPP, lane 63's from its own load of the next vector (no
+// LDS, no workgroup barrier); BS-thread workgroups so the extra load hits the line a sibling wave
+// of the same workgroup (same CU, same L2) fetches.  SERIAL: source 1's load after source 0's landed.
+template <int NS, int BS, bool SERIAL, bool XCD>
+__global__ __launch_bounds__(BS) void k_wedge(Args a)
+{
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint64_t i0 = lblock(blockIdx.x, gridDim.x, XCD) * BS;
+    if (i0 >= a.nitems) return;
+    const uint64_t wo = i0 * 16;
+    u32x4 acc;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const auto r = rsrc(uptr(a.s[j] + wo));
+        const u32x4 A = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0, kNT);
+        u32x4 E = A;
+        if (lane == 63) E = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u + 16u, 0, kNT);
+        if (SERIAL && j == 0 && NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        u32x4 B;
+        B.x = __builtin_amdgcn_update_dpp(0u, A.x, 0x130, 0xF, 0xF, false);
+        B.y = __builtin_amdgcn_update_dpp(0u, A.y, 0x130, 0xF, 0xF, false);
+        B.z = __builtin_amdgcn_update_dpp(0u, A.z, 0x130, 0xF, 0xF, false);
+        B.w = __builtin_amdgcn_update_dpp(0u, A.w, 0x130, 0xF, 0xF, false);
+        if (lane == 63) B = E;
+        const u32x4 x = funnel16(A, B, a.k);
+        acc = j == 0 ? x : addv(acc, x);
+    }
+    if (i0 + tid < a.nitems) wt(uptr(a.d + wo), tid * 16u, acc);
+}
+
+// Round 6: unaligned 16-B buffer loads (the phased reduce-scatter's shifted path) in BS-thread
+// workgroups, optionally XCD-grouped, SERIAL as above.
+template <int NS, int BS, bool SERIAL, bool XCD>
+__global__ __launch_bounds__(BS) void k_unalw(Args a)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i0 = lblock(blockIdx.x, gridDim.x, XCD) * BS;
+    if (i0 + tid >= a.nitems) return;
+    const uint64_t wo = i0 * 16;
+    u32x4 acc = __builtin_amdgcn_raw_buffer_load_b128(rsrc(uptr(a.s[0] + a.k + wo)), tid * 16u, 0, kNT);
+    if (SERIAL && NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (NS == 2) acc = addv(acc, __builtin_amdgcn_raw_buffer_load_b128(rsrc(uptr(a.s[1] + a.k + wo)), tid * 16u, 0, kNT));
+    wt(uptr(a.d + wo), tid * 16u, acc);
+}
+
 // The product's kernels with FaninArgs built as runtime.cpp plan_fanin builds them.
 static ishmemi::FaninArgs prod_args(const Args &a, int ns, bool aligned)
 {
@@ -395,10 +440,23 @@ int main(int argc, char **argv)
     CK(hipMemcpy(s1, h1.data(), bytes + 4096, hipMemcpyHostToDevice));
     std::vector<Variant> vs = {
         {"copy product aligned", 1, 64, 64, true, nullptr, 1},
-        {"a+b al 64x1 sc01", 2, 64, 64, true, k_al<2, 64, 1, 17>},
-        {"a+b al 64x1 serial", 2, 64, 64, true, k_al<2, 64, 1, 17, true>},
+        {"copy product realign", 1, 512, 512, false, nullptr, 2},
+        {"copy wedge 512", 1, 512, 512, false, k_wedge<1, 512, false, false>},
+        {"copy wedge 256", 1, 256, 256, false, k_wedge<1, 256, false, false>},
+        {"copy wedge 1024", 1, 1024, 1024, false, k_wedge<1, 1024, false, false>},
+        {"copy wedge 64 xcd", 1, 64, 64, false, k_wedge<1, 64, false, true>},
+        {"copy unal 64 xcd", 1, 64, 64, false, k_unalw<1, 64, false, true>},
+        {"copy unal 512", 1, 512, 512, false, k_unalw<1, 512, false, false>},
         {"a+b product aligned", 2, 64, 64, true, nullptr, 1},
         {"a+b product realign", 2, 512, 512, false, nullptr, 2},
+        {"a+b wedge 512", 2, 512, 512, false, k_wedge<2, 512, false, false>},
+        {"a+b wedge 512 serial", 2, 512, 512, false, k_wedge<2, 512, true, false>},
+        {"a+b wedge 256 serial", 2, 256, 256, false, k_wedge<2, 256, true, false>},
+        {"a+b wedge 64 xcd serial", 2, 64, 64, false, k_wedge<2, 64, true, true>},
+        {"a+b unal 64 (rs now)", 2, 64, 64, false, k_unalw<2, 64, false, false>},
+        {"a+b unal 64 xcd", 2, 64, 64, false, k_unalw<2, 64, false, true>},
+        {"a+b unal 64 xcd serial", 2, 64, 64, false, k_unalw<2, 64, true, true>},
+        {"a+b unal 512 serial", 2, 512, 512, false, k_unalw<2, 512, true, false>},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
