@@ -1010,7 +1010,13 @@ int reduce_heap(State &s, int team, int op, int dt, void *dst, const void *src, 
         ph.me = t.my_idx;
         ph.peer_nt = s.phased_peer_nt;
         ph.whole = direct ? 1 : 0;
-        ph.xcd_group = s.rs_xcd;
+        // XCD-grouped block order for shifted sources: only when this PE has its GPU to itself.  The
+        // order assumes workgroup b runs on XCD b mod 8, which holds for a kernel running alone (1 GiB
+        // a + b from sources 4 / 12 B off: 0.75 -> 0.83 of HBM, one process); with co-located PEs'
+        // grids dispatched together it does not (2 / 4 PEs x 1 GiB, sources 4 B off: reduce-scatter
+        // grid 0.524-0.537 ms either way, profiles/r06/realign/r06c_ab.txt).  Block order only: no
+        // member pairs with another's blocks, so PEs may differ.
+        ph.xcd_group = s.rs_xcd && device_share() == 1 ? 1 : 0;
         if (inplace_fold) ph.dst = scratch;
         if (realign) {
             const uint64_t h = std::min<uint64_t>(n, ((16 - d0 % 16) % 16) / es);
