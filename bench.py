@@ -799,6 +799,14 @@ def main() -> int:
     if world != args.gpus:
         raise RuntimeError(f"--gpus {args.gpus} but the launcher started {world} ranks")
     same_device = os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1"
+    # ISHMEM_BENCH_EMULATE_SHARE1=1 with ISHMEM_BENCH_SAME_DEVICE=1 (development only): every rank
+    # reports its own device (the test-hooks library's ISHMEM_TEST_PCI_BUS), so the team counts as
+    # one PE per GPU — the cross-device thresholds, launch shapes and `recommended` keys of the node
+    # — while the ranks still share this box's one GPU.  Never used for reported numbers.
+    emulate_share1 = same_device and os.environ.get("ISHMEM_BENCH_EMULATE_SHARE1") == "1"
+    if emulate_share1:
+        os.environ["ISHMEM_TEST_PCI_BUS"] = f"fake-bus-{rank}"
+        os.environ.setdefault("ISHMEM_AMD_LIB", str(ROOT / "ishmem_amd" / "libishmem_amd_testhooks.so"))
     n = args.nelems if args.nelems > 0 else (args.mib << 20) // 4
     B = n * 4
     sweep_max = min(args.sweep_max_mib << 20, CFG5_MAX_BYTES)
@@ -1040,7 +1048,8 @@ def main() -> int:
             "kernel_ms": kern_ms, "checked": checked, "targets": targets,
             **({"flag_memory": flag_memory} if world > 1 else {}),
             **({"topology": link_topology(hip, device, world)} if world > 1 and not same_device else {}),
-            **({"dev_same_device": True} if same_device else {}), "roofline": roof,
+            **({"dev_same_device": True} if same_device else {}),
+            **({"dev_emulated_one_pe_per_gpu": True} if emulate_share1 else {}), "roofline": roof,
             "cpu_baseline": cpu, **extra,
         }
     if world > 1 and not args.no_rccl and not same_device:

@@ -270,31 +270,40 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
  * ishmemi_c_set_param names: "max_blocks" (workgroups per collective launch, <= 1024),
  * "ll_max_bytes" (cap on the one-hop granule path, default 524288, <= 1048576; the path also stops
  * at the team's ring capacity, 2 MiB / team size: get_param "ll_capacity_bytes" for TEAM_WORLD),
- * "timeout_ms" (bound on every
- * device-side spin), "stream_order" (1: collectives issued on different streams are ordered by
- * the library in call order, ~2 us per call; 0, the default: the caller orders them, as the
- * reference requires), "oneshot_p2_max_bytes" (two-member teams: one-phase fold up to this size,
- * default 32 MiB), "direct_p2" (1, default: that fold as barrier + one grid + barrier; 0: the
- * persistent kernel's one-shot mode), "phased_min_bytes" (payloads of at least this size take the phased path:
+ * "timeout_ms" (bound on every device-side spin), "stream_order" (1: collectives issued on
+ * different streams are ordered by the library in call order, ~2 us per call; 0, the default: the
+ * caller orders them, as the reference requires), "oneshot_p2_max_bytes" (co-located two-member
+ * teams: one-phase fold up to this size, default 32 MiB; 3-4 members: oneshot_p2 / 4 / (p - 1)),
+ * "direct_p2" (1, default: that fold as barrier + one grid + barrier; 0: the persistent kernel's
+ * one-shot mode), "phased_min_bytes" (payloads of at least this size take the phased path:
  * barrier, one-shot reduce-scatter, barrier, one-shot all-gather, barrier; -1 disables it),
- * "phase_events" (1: the next phased reduces record HIP events between their five launches, read
- * with ishmemi_c_phase_times; a measurement hook), "debug"; A/B switches for measurements, set
- * alike on every PE: "ar_shifted" (1, default: the persistent kernel keeps 16-B items for sources on
- * another 16-B phase than dest, read with unaligned loads; 0: element-granular), "phase_unaligned"
- * (1, default: the phased reduce-scatter reads such sources with unaligned 16-B loads; 0: the
- * realigning kernel), "collect_realign" (1, default: collect members off the 16-B grid realigned;
- * 0: narrow items), "barrier_kind" (0 kernel, 1 stream memory operations), "block_spin" (blocking
- * calls' wait: 2, default, spin on a stream-written host word; 1 the spin then
- * hipStreamSynchronize; 0 hipStreamSynchronize), "direct_max_pes" (largest team taking the
- * whole-array fold, default 4), "direct_inplace" (1, default: in-place calls with p * B <= 4 MiB
- * fold into a team-private scratch and copy back).  "ll_max_bytes",
- * "oneshot_p2_max_bytes" and "phased_min_bytes" choose the kernels of a multi-PE call: init
- * agrees on them (the minimum over the PEs; the maximum for "phased_min_bytes") and a later
- * set_param must be made with the same value on every PE.  "max_blocks" may differ between PEs (the kernels grab work,
- * nothing is paired by workgroup index).  ishmemi_c_get_param also reports "staging_bytes",
- * "heap_bytes", "flags_fine_grained", "ll_capacity_bytes" / "ll_limit_bytes" (TEAM_WORLD's granule
- * ring capacity / threshold), "cu_count" (compute units of this PE's device) and
- * "device_share" (PEs of the job on this PE's device: 1 with one PE per GPU). */
+ * "xgmi_ll_max_bytes" / "xgmi_fold_max_bytes" (teams whose members sit on different GPUs: the
+ * granule-path / whole-array fold thresholds, -1 = the link-byte model of ishmemi_c_path_limits;
+ * ISHMEM_XGMI_LL_MAX_BYTES / ISHMEM_XGMI_FOLD_MAX_BYTES at init), "xgmi_link_mbps" (the model's
+ * link rate per direction, default 76800), "phase_events" (1: the next phased reduces record HIP
+ * events between their five launches, read with ishmemi_c_phase_times; a measurement hook),
+ * "debug"; A/B switches for measurements, set alike on every PE: "ar_shifted" (1, default: the
+ * persistent kernel keeps 16-B items for sources on another 16-B phase than dest, read with
+ * unaligned loads; 0: element-granular), "phase_unaligned" (1, default: the phased reduce-scatter
+ * reads such sources with unaligned 16-B loads; 0: the realigning kernel), "rs_xcd" (1, default:
+ * that reduce-scatter's XCD-grouped block order when the PE has its GPU to itself; 0: block
+ * order), "collect_realign" (1, default: collect members off the 16-B grid realigned; 0: narrow
+ * items), "block_spin" (blocking calls' wait: 2, default, spin on a stream-written host word; 1 the
+ * spin then hipStreamSynchronize; 0 hipStreamSynchronize), "direct_max_pes" (largest team taking
+ * the whole-array fold, default 4), "direct_inplace" (1, default: in-place calls with p * B <= 4 MiB
+ * fold into the team's private scratch, allocated with the team, and copy back).  The thresholds
+ * choose the kernels of a multi-PE call: init agrees on them (the minimum over the PEs; the
+ * maximum for "phased_min_bytes") and a later set_param must be made with the same value on every
+ * PE.  "max_blocks" may differ between PEs (the kernels grab work, nothing is paired by workgroup
+ * index).  ishmemi_c_get_param also reports "staging_bytes", "heap_bytes", "flags_fine_grained",
+ * "ll_capacity_bytes" / "ll_limit_bytes" / "fold_limit_bytes" (TEAM_WORLD's granule ring capacity,
+ * granule threshold and whole-array fold bound), "team_colocated" (1: every TEAM_WORLD member on
+ * one GPU), "teams_max" (ISHMEM_TEAMS_MAX, default 64), "flag_block_bytes" (flag memory this PE
+ * holds: the base block plus one block per split team it belongs to; "flag_block_bytes_round5" =
+ * round 5's fixed 16-slot block, for comparison), "init_us_<phase>" (init's phases: hip, heap,
+ * flags, bootstrap, ipc_heap, ipc_flags, teams, total; printed under ISHMEM_DEBUG=2), "cu_count"
+ * (compute units of this PE's device) and "device_share" (PEs of the job on this PE's device: 1
+ * with one PE per GPU). */
 const char *ishmemi_c_last_error(void);
 int ishmemi_c_set_param(const char *name, long long value);
 long long ishmemi_c_get_param(const char *name);

@@ -43,6 +43,11 @@ for s in $STEPS; do
             np_=${s#local}
             ISHMEM_BENCH_SAME_DEVICE=1 run bench_$s 900 python bench.py --gpus $np_ --steps 10 --warmup 3 \
                 --mib ${MIB:-1024} --sweep-max-mib ${SWEEP_MIB:-4096} ;;
+    elocal2|elocal4|elocal8)  # the same rehearsal with every rank on its own emulated GPU (test-hooks
+            # library): the cross-device thresholds and `recommended` keys of one PE per GPU
+            np_=${s#elocal}
+            ISHMEM_BENCH_SAME_DEVICE=1 ISHMEM_BENCH_EMULATE_SHARE1=1 run bench_$s 900 python bench.py --gpus $np_ \
+                --steps 10 --warmup 3 --mib ${MIB:-1024} --sweep-max-mib ${SWEEP_MIB:-256} --no-e2e --no-rccl ;;
     sweep1) run sweep1 300 python tools/sweep.py --max-mib 1024 ;;
     bw2)    # tests/cpp/reduce_bw.cpp at 2 PEs (all modes incl. device_multi_wg 1/2/4/8 groups), CSV
             key=bw$RANDOM$RANDOM
