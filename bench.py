@@ -86,6 +86,25 @@ def host_info() -> dict:
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+def stall_report(what: str) -> None:
+    """Where a stalled setup step is: the Python stack of every thread and, per
+    native thread, its name, kernel wait channel and current syscall (/proc: nothing attaches to the
+    process), on stderr.  Called by a timer; the run continues (or is ended by its own limit)."""
+    import faulthandler
+    rank = os.environ.get("RANK", "0")
+    print(f"[bench rank {rank}] {what} has not finished after its watchdog interval; thread states:",
+          file=sys.stderr, flush=True)
+    faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+    for t in sorted(Path("/proc/self/task").iterdir(), key=lambda x: int(x.name)):
+        def rd(n):
+            try:
+                return (t / n).read_text().strip().replace("\n", " ")
+            except OSError:
+                return "?"
+        print(f"[bench rank {rank}]   tid {t.name} comm={rd('comm')} wchan={rd('wchan')} syscall={rd('syscall')[:60]}",
+              file=sys.stderr, flush=True)
+
+
 def self_launch(args) -> int:
     """--gpus N > 1 without a launcher: run the N ranks as a child torch.distributed.run (never
     exec: nothing here has touched the GPU, and the parent only relays), rank 0's JSON line
@@ -823,6 +842,11 @@ def main() -> int:
         dist.broadcast_object_list(obj, src=0)
         key = obj[0]
 
+    import threading
+    watchdog = threading.Timer(float(os.environ.get("ISHMEM_BENCH_SETUP_WATCHDOG_S", "45")), stall_report,
+                               args=("setup (library load, ishmem init, heap allocation, input upload)",))
+    watchdog.daemon = True
+    watchdog.start()
     import ishmem_amd as ish
     from ishmem_amd import hip
 
@@ -853,6 +877,7 @@ def main() -> int:
         if r != 0:
             raise RuntimeError(f"reduce failed: {ish.last_error()}")
 
+    watchdog.cancel()
     log("warm-up")
     for _ in range(args.warmup):
         step()

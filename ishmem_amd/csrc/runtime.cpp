@@ -254,7 +254,7 @@ void warn_unknown_env()
         "STAGED_COPY_KERNEL", "STREAM_ORDER", "FLAGS_KIND", "EP_UNCACHED", "BARRIER_KIND", "XGMI_LL_MAX_BYTES",
         "XGMI_FOLD_MAX_BYTES", "TEST_FLAGS_UNAVAILABLE", "TEST_PCI_BUS",
         // the Python package, build and bench harness
-        "AMD_LIB", "OFFLOAD_ARCH", "BENCH_SAME_DEVICE"};
+        "AMD_LIB", "OFFLOAD_ARCH", "BENCH_SAME_DEVICE", "BENCH_EMULATE_SHARE1", "BENCH_SETUP_WATCHDOG_S"};
     for (char **e = ::environ; e && *e; ++e) {
         if (strncmp(*e, "ISHMEM_", 7) != 0) continue;
         const char *name = *e + 7, *eq = strchr(name, '=');
@@ -1864,12 +1864,22 @@ int init_impl(int pe, int npes, int device, const std::string &key)
     using clk = std::chrono::steady_clock;
     const auto t_start = clk::now();
     auto t_mark = t_start;
+    // Under ISHMEM_DEBUG=2 every phase prints as it ends, so a stalled init shows where it is.
     auto phase_done = [&](int k) {
         const auto now = clk::now();
         s.init_us[k] = std::chrono::duration<double, std::micro>(now - t_mark).count();
         t_mark = now;
+        if (s.debug > 1) {
+            fprintf(stderr, "[ishmem_amd] PE %d init: %s done (%.1f ms)\n", pe, kInitPhase[k], s.init_us[k] / 1000.0);
+            fflush(stderr);
+        }
     };
     for (double &u : s.init_us) u = 0;
+    if (s.debug > 1) {
+        fprintf(stderr, "[ishmem_amd] PE %d of %d init: start (device %d, heap %zu MiB, key '%s')\n", pe, npes, device,
+                heap_request >> 20, key.c_str());
+        fflush(stderr);
+    }
 
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
