@@ -33,6 +33,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 import uuid
 from pathlib import Path
@@ -833,6 +834,24 @@ def main() -> int:
         # The config-5 sweep holds a 4 GiB source and dest per PE (plus the 128 MiB staging
         # region): size the symmetric heap for it (288 GB of HBM per GPU).
         os.environ["ISHMEM_SYMMETRIC_SIZE"] = str(max(2 * B, 2 * sweep_max) + (1 << 30))
+    # The library and the ctypes HIP bindings are loaded BEFORE torch: torch ships its own copy of
+    # the HIP / HSA runtime (ROCm 7.0, same sonames as the image's 7.2), and whichever loads first
+    # serves the whole process.  Loaded first, the image's runtime serves the library, the bindings
+    # and torch alike — the configuration every GPU test runs in.  With torch first, the library
+    # ran on torch's copy, and the 2-PE rehearsal that was a box's first GPU process stalled inside
+    # hipIpcOpenMemHandle of the peer's heap (the setup watchdog's thread dump, profiles/r06/init/
+    # r06f_bench_local2_stall.txt), as round 5's r05zm run had stalled after HIP's start.
+    watchdog = threading.Timer(float(os.environ.get("ISHMEM_BENCH_SETUP_WATCHDOG_S", "45")), stall_report,
+                               args=("setup (library load, ishmem init, heap allocation, input upload)",))
+    watchdog.daemon = True
+    watchdog.start()
+    import ishmem_amd as ish
+    from ishmem_amd import hip
+    hip.lib()
+    try:  # and the image's HSA runtime under the name torch's HIP-side libraries ask for
+        ctypes.CDLL("libhsa-runtime64.so", mode=ctypes.RTLD_GLOBAL)
+    except OSError:
+        pass
     dist = None
     key = f"bench{uuid.uuid4().hex[:10]}"
     if world > 1:
@@ -842,13 +861,6 @@ def main() -> int:
         dist.broadcast_object_list(obj, src=0)
         key = obj[0]
 
-    import threading
-    watchdog = threading.Timer(float(os.environ.get("ISHMEM_BENCH_SETUP_WATCHDOG_S", "45")), stall_report,
-                               args=("setup (library load, ishmem init, heap allocation, input upload)",))
-    watchdog.daemon = True
-    watchdog.start()
-    import ishmem_amd as ish
-    from ishmem_amd import hip
 
     # ISHMEM_BENCH_SAME_DEVICE=1 (development only): every rank on device 0, to measure kernel
     # overheads of the multi-PE path on a one-GPU box.  Never used for reported numbers.

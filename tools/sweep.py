@@ -6,6 +6,7 @@ bytes, us per call (max over ranks), algbw GiB/s.  Results are checked against t
 from __future__ import annotations
 
 import argparse
+import ctypes
 import os
 import sys
 import uuid
@@ -44,6 +45,19 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     key = f"sw{uuid.uuid4().hex[:10]}"
+    if args.emulate_share1:
+        os.environ["ISHMEM_TEST_PCI_BUS"] = f"fake-bus-{rank}"
+        # The test-hooks build unless an A/B variant (built with ISHMEMI_TEST_HOOKS) is named.
+        os.environ.setdefault("ISHMEM_AMD_LIB", str(Path(__file__).resolve().parents[1] / "ishmem_amd/libishmem_amd_testhooks.so"))
+    # The library (and the image's HIP runtime with it) before torch, whose own HIP copy would
+    # otherwise serve the process (bench.py main, round 6).
+    import ishmem_amd as ish
+    from ishmem_amd import hip
+    hip.lib()
+    try:  # and the image's HSA runtime under the name torch's HIP-side libraries ask for
+        ctypes.CDLL("libhsa-runtime64.so", mode=ctypes.RTLD_GLOBAL)
+    except OSError:
+        pass
     if world > 1:
         import torch
         import torch.distributed as dist
@@ -51,12 +65,6 @@ def main() -> None:
         obj = [key]
         dist.broadcast_object_list(obj, src=0)
         key = obj[0]
-    if args.emulate_share1:
-        os.environ["ISHMEM_TEST_PCI_BUS"] = f"fake-bus-{rank}"
-        # The test-hooks build unless an A/B variant (built with ISHMEMI_TEST_HOOKS) is named.
-        os.environ.setdefault("ISHMEM_AMD_LIB", str(Path(__file__).resolve().parents[1] / "ishmem_amd/libishmem_amd_testhooks.so"))
-    import ishmem_amd as ish
-    from ishmem_amd import hip
     dev = 0 if os.environ.get("ISHMEM_BENCH_SAME_DEVICE") == "1" else local
     ish.init(rank, world, dev, key)
     for kv in args.param:
