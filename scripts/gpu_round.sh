@@ -30,7 +30,8 @@ for s in $STEPS; do
     smoke)  run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
     init)   # init time by phase at 2 PEs, heap 1 / 4 / 9 GiB then 1 GiB again (the first run is the
             # box's first HIP process: cold), ISHMEM_DEBUG=2 phase lines on stderr
-            run init_timing 400 python tools/init_timing.py --npes 2 --sizes ${INIT_SIZES:-1G,4G,9G,1G} ;;
+            run init_timing 400 python tools/init_timing.py --npes ${INIT_NPES:-2} --sizes ${INIT_SIZES:-1G,4G,9G,1G} \
+                --splits ${INIT_SPLITS:-0} ;;
     gpu)    run pytest_gpu 1500 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider ;;
     sel)    run pytest_sel ${SEL_SECS:-1500} python -u -m pytest tests -m gpu -x -v --timeout ${SEL_TIMEOUT:-900} \
                 --timeout-method thread -p no:cacheprovider -k "$SEL" ;;

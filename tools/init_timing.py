@@ -23,7 +23,7 @@ ROOT = Path(__file__).resolve().parents[1]
 PHASES = ("hip", "heap", "flags", "bootstrap", "ipc_heap", "ipc_flags", "teams", "total")
 
 
-def pe_main(pe, npes, key, size, q, t_spawn):
+def pe_main(pe, npes, key, size, q, t_spawn, splits=0):
     t_start = time.time()
     os.environ["ISHMEM_SYMMETRIC_SIZE"] = size
     os.environ.setdefault("ISHMEM_DEBUG", "2")
@@ -42,6 +42,19 @@ def pe_main(pe, npes, key, size, q, t_spawn):
            "import_ms": round((t_imported - t_start) * 1e3, 1), "err": err}
     if ok:
         rec["phases_ms"] = {p: round(ish.get_param(f"init_us_{p}") / 1e3, 2) for p in PHASES}
+        if splits:
+            # team_split_strided of WORLD `splits` times (each allocates, exports, exchanges and
+            # opens the new team's flag block), then team_destroy of them all: ms per team
+            ish.ishmem_barrier_all()
+            t1 = time.perf_counter()
+            teams = [ish.ishmem_team_split_strided(0, 0, 1, npes)[1] for _ in range(splits)]
+            t2 = time.perf_counter()
+            for t in teams:
+                ish.ishmem_team_destroy(t)
+            t3 = time.perf_counter()
+            rec["split_ms_per_team"] = round((t2 - t1) * 1e3 / splits, 3)
+            rec["destroy_ms_per_team"] = round((t3 - t2) * 1e3 / splits, 3)
+            rec["teams_ok"] = sum(t >= 0 for t in teams)
         ish.ishmem_barrier_all()
         ish.ishmem_finalize()
     q.put(rec)
@@ -52,6 +65,7 @@ def main() -> int:
     ap.add_argument("--npes", type=int, default=2)
     ap.add_argument("--sizes", default="1G,4G,9G,1G")
     ap.add_argument("--timeout", type=float, default=120.0)
+    ap.add_argument("--splits", type=int, default=0, help="also time this many team splits + destroys (<= 61)")
     args = ap.parse_args()
     ctx = mp.get_context("spawn")
     rc = 0
@@ -59,7 +73,7 @@ def main() -> int:
         q = ctx.Queue()
         key = f"it{uuid.uuid4().hex[:10]}"
         t_spawn = time.time()
-        procs = [ctx.Process(target=pe_main, args=(pe, args.npes, key, size, q, t_spawn)) for pe in range(args.npes)]
+        procs = [ctx.Process(target=pe_main, args=(pe, args.npes, key, size, q, t_spawn, args.splits)) for pe in range(args.npes)]
         for p in procs:
             p.start()
         got = []
