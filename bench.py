@@ -329,8 +329,8 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
       phased_peer_nt - 64 MiB and the payload on the phased path with nontemporal peer loads
                (the collectives issue sc0 sc1 ones; the tripwire_peer_nt leg checks coherence);
       p2    - two PEs: one-shot fold vs reduce-scatter + all-gather at the payload size;
-      fold  - 512 KiB - 4 MiB: the whole-array fold between two barriers forced for this team
-              size against the path without it (granule path off in both);
+      fold  - 512 KiB - 4 MiB (2 PEs: to 64 MiB): the whole-array fold between two barriers forced
+              for this team size against the path without it (granule path off in both);
       ll    - 4 KiB up to the granule ring's capacity (2 MiB / team size) with the one-hop granule
               path on (default) and off."""
 
@@ -386,7 +386,10 @@ def xgmi_tuning(ish, hip, src, dst, B, world, dist, stream):
     # The whole-array fold (two barriers around one grid in which every member folds every
     # member's source) against the default path below it, at mid sizes: decided on one GPU for
     # 2-4 PEs; over xGMI each member pulls (p - 1) * B instead of 2(p - 1)/p * B.
-    for nb in (512 << 10, 1 << 20, 2 << 20, 4 << 20):
+    # Two members: up to 64 MiB as well, so the crossover with reduce-scatter + all-gather is
+    # bracketed by measured sizes (the `recommended` block reads the largest size the fold won).
+    fold_sizes = [512 << 10, 1 << 20, 2 << 20, 4 << 20] + ([8 << 20, 16 << 20, 32 << 20, 64 << 20] if world == 2 else [])
+    for nb in fold_sizes:
         if nb <= B:
             run("fold", "direct_max_pes", max(2, world), nb, 20,
                 also={"direct_p2": 1, "oneshot_p2_max_bytes": 1 << 40, "xgmi_fold_max_bytes": 1 << 40,
