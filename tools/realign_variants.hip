@@ -317,6 +317,34 @@ __global__ __launch_bounds__(BS) void k_unalw(Args a)
     wt(uptr(a.d + wo), tid * 16u, acc);
 }
 
+// Round 6: items laid out by the SOURCES' phase instead — aligned 16-B source loads, the store
+// unaligned (dest + 16 - k + 16 i); the first 16 - k bytes and the last item are not written
+// (the check skips them).  SC1: source 1 loaded system-coherent (sc0 sc1), as a peer source is.
+template <int NS, bool XCD, bool SC1>
+__global__ __launch_bounds__(64) void k_stshift(Args a)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i0 = lblock(blockIdx.x, gridDim.x, XCD) * 64;
+    if (i0 + tid + 1 >= a.nitems) return;
+    const uint64_t wo = (i0 + 1) * 16;  // source bytes from s[j] (aligned)
+    u32x4 acc = __builtin_amdgcn_raw_buffer_load_b128(rsrc(uptr(a.s[0] + wo)), tid * 16u, 0, kNT);
+    if (NS == 2) acc = addv(acc, __builtin_amdgcn_raw_buffer_load_b128(rsrc(uptr(a.s[1] + wo)), tid * 16u, 0, SC1 ? 17 : kNT));
+    __builtin_amdgcn_raw_buffer_store_b128(acc, rsrc(uptr(a.d + wo - a.k)), tid * 16u, 0, kSC);
+}
+
+// The reduce-scatter's current shifted shape with source 1 system-coherent (its peer), for k_stshift.
+template <int NS, bool XCD>
+__global__ __launch_bounds__(64) void k_unal_sc(Args a)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i0 = lblock(blockIdx.x, gridDim.x, XCD) * 64;
+    if (i0 + tid >= a.nitems) return;
+    const uint64_t wo = i0 * 16;
+    u32x4 acc = __builtin_amdgcn_raw_buffer_load_b128(rsrc(uptr(a.s[0] + a.k + wo)), tid * 16u, 0, kNT);
+    if (NS == 2) acc = addv(acc, __builtin_amdgcn_raw_buffer_load_b128(rsrc(uptr(a.s[1] + a.k + wo)), tid * 16u, 0, 17));
+    wt(uptr(a.d + wo), tid * 16u, acc);
+}
+
 // The product's kernels with FaninArgs built as runtime.cpp plan_fanin builds them.
 static ishmemi::FaninArgs prod_args(const Args &a, int ns, bool aligned)
 {
@@ -457,6 +485,11 @@ int main(int argc, char **argv)
         {"a+b unal 64 xcd", 2, 64, 64, false, k_unalw<2, 64, false, true>},
         {"a+b unal 64 xcd serial", 2, 64, 64, false, k_unalw<2, 64, true, true>},
         {"a+b unal 512 serial", 2, 512, 512, false, k_unalw<2, 512, true, false>},
+        {"a+b unal 64 nt+sc", 2, 64, 64, false, k_unal_sc<2, false>},
+        {"a+b stshift 64 nt+sc", 2, 64, 64, false, k_stshift<2, false, true>},
+        {"a+b stshift 64 nt+nt", 2, 64, 64, false, k_stshift<2, false, false>},
+        {"a+b stshift 64 xcd nt+sc", 2, 64, 64, false, k_stshift<2, true, true>},
+        {"copy stshift 64", 1, 64, 64, false, k_stshift<1, false, false>},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
@@ -474,7 +507,9 @@ int main(int argc, char **argv)
         CK(hipMemcpy(got.data(), d, bytes, hipMemcpyDeviceToHost));
         const uint32_t k = a.k;
         uint64_t bad = 0;
+        const bool st = vs[v].name.find("stshift") != std::string::npos;
         for (uint64_t w = 0; w < n * 4; ++w) {
+            if (st && (4 * w < 16 - k || 4 * w + 4 > 16 * (n - 1) + 16 - k)) continue;
             uint32_t e0w, e1w;
             memcpy(&e0w, (const char *) h.data() + k + 4 * w, 4);
             memcpy(&e1w, (const char *) h1.data() + k + 4 * w, 4);
