@@ -111,4 +111,21 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _lib = lib
+    _warn_foreign_runtime()
     return lib
+
+
+def _warn_foreign_runtime() -> None:
+    """torch ships its own HIP runtime under the image's soname; when torch was imported first, that
+    copy serves this library too.  Every GPU test runs on the image's runtime, and the round-6 N > 1
+    rehearsals stalled in the heap's IPC import on torch's copy, so say so once."""
+    try:
+        with open("/proc/self/maps") as f:
+            foreign = any("amdhip64" in line and "/torch/lib/" in line for line in f)
+    except OSError:
+        return
+    if foreign:
+        import sys
+        print("[ishmem_amd] WARN: the HIP runtime in use is torch's bundled copy (torch was imported "
+              "before ishmem_amd); import ishmem_amd first so the image's runtime serves the process",
+              file=sys.stderr, flush=True)
