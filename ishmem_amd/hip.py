@@ -99,6 +99,13 @@ def synchronize() -> None:
     _check(lib().hipDeviceSynchronize(), "hipDeviceSynchronize")
 
 
+def mem_get_info() -> tuple[int, int]:
+    """(free, total) bytes of the current device (hipMemGetInfo)."""
+    free, total = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    _check(lib().hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)), "hipMemGetInfo")
+    return free.value, total.value
+
+
 def stream_create() -> int:
     s = ctypes.c_void_p()
     _check(lib().hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1)), "hipStreamCreate")

@@ -164,6 +164,73 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             ish.ishmem_free(d_t)
             ish.ishmem_free(s_t)
 
+        if "teamchurn" in scenarios:
+            # Team churn (round 6): every split allocates, exports and opens a team block, every
+            # destroy closes and frees it.  CHURN_ITERS rounds of: split a random strided team of
+            # WORLD (and a nested one inside it), reduce on both (random op / type / size up to the
+            # fold sizes) against the oracle, destroy both in a random order.  The footprint must
+            # come back to the base block, and the device's free memory must not drift (leaked
+            # blocks or IPC mappings would show as a steady drop).
+            import random
+            rng = random.Random(int(os.environ.get("CHURN_SEED", 4242)))
+            iters = int(os.environ.get("CHURN_ITERS", 120))
+            W, INV = ish.ISHMEM_TEAM_WORLD, ish.ISHMEM_TEAM_INVALID
+            fb0 = int(ish.get_param("flag_block_bytes"))
+            nmax = 600_000
+            s_c, d_c = heap(nmax, DT["double"]), heap(nmax, DT["double"])
+            ish.ishmem_barrier_all()
+            hip.synchronize()
+            free0 = hip.mem_get_info()[0]
+            for it in range(iters):
+                # the same draws on every PE (shared seed)
+                stride = rng.choice([1, 1, 2, 3]) if npes >= 3 else 1
+                size = rng.randint(1, (npes - 1) // stride + 1)
+                start = rng.randint(0, npes - 1 - stride * (size - 1))
+                op_n = rng.choice(["sum", "max", "min", "prod", "and", "xor"])
+                dt_n = rng.choice(["int32", "int64", "uint8", "float", "double"]) if op_n not in ("and", "xor") else rng.choice(["int32", "uint8", "int64"])
+                n = rng.choice([1, 37, 4099, 70_001, 300_000, nmax // 2])
+                order = rng.random() < 0.5
+                r, t = ish.ishmem_team_split_strided(W, start, stride, size)
+                members = [start + k * stride for k in range(size)]
+                if r or (t != INV) != (pe in members):
+                    fails.append(f"pe{pe} churn {it}: split ({start},{stride},{size}) rc={r} team={t} {ish.last_error()}")
+                    break
+                t2 = INV
+                if t != INV and size >= 2:
+                    r2, t2 = ish.ishmem_team_split_strided(t, 0, 1, size - 1)
+                    if r2 or (t2 != INV) != (members.index(pe) < size - 1):
+                        fails.append(f"pe{pe} churn {it}: nested split rc={r2} team={t2} {ish.last_error()}")
+                        break
+                for tm, mem in ((t, members), (t2, members[:size - 1])):
+                    if tm == INV:
+                        continue
+                    op, dt = OPS[op_n], DT[dt_n]
+                    if not ish.lib().ishmemi_c_op_dtype_valid(op, dt):
+                        continue
+                    ins = {j: oracle.fill_random(dt, 7700 + 13 * it + j, n) for j in mem}
+                    hip.upload(s_c, ins[pe])
+                    if ish.reduce(op_n, dt_n, d_c, s_c, n, tm):
+                        fails.append(f"pe{pe} churn {it}: reduce {op_n} {dt_n} n={n} team {tm}: {ish.last_error()}")
+                        continue
+                    check(f"churn {it} {op_n} {dt_n} n={n}", op, dt, [ins[j] for j in mem],
+                          hip.download(d_c, n, oracle.NP[dt]), me=mem.index(pe))
+                for tm in ((t2, t) if order else (t, t2)):
+                    if tm != INV:
+                        ish.ishmem_team_destroy(tm)
+                if fails:
+                    break
+            ish.ishmem_barrier_all()
+            hip.synchronize()
+            fb = int(ish.get_param("flag_block_bytes"))
+            free1 = hip.mem_get_info()[0]
+            if fb != fb0:
+                fails.append(f"pe{pe} churn: flag footprint {fb} after {iters} split / destroy rounds, base {fb0}")
+            # One team block is 8.25 MiB; a leak of one per round would lose iters x 8.25 MiB.
+            if free0 - free1 > (64 << 20):
+                fails.append(f"pe{pe} churn: device free memory fell by {(free0 - free1) >> 20} MiB over {iters} rounds")
+            ish.ishmem_free(d_c)
+            ish.ishmem_free(s_c)
+
         if "inplacegraph" in scenarios:
             # the in-place whole-array fold's path no longer depends on stream
             # capture (its scratch is allocated with the team).  PE 0 captures an in-place f32 sum

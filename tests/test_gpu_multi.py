@@ -426,3 +426,11 @@ def test_coarse_grained_flags_across_devices_refused_at_init(forced):
     if forced:
         env["ISHMEM_FLAGS_KIND"] = 2
     run_pes(2, ["refuse"], env=env, timeout=120)
+
+
+@pytest.mark.parametrize("npes", [2, 3, 4])
+def test_team_churn_split_destroy_memory_stable(npes):
+    # Round 6: split / reduce / destroy of random strided teams and nested teams, 120 rounds, every
+    # result vs the oracle; the flag footprint returns to the base block and the device's free
+    # memory does not drift (each split allocates, exports and maps a team block).
+    run_pes(npes, ["teamchurn"], env={"CHURN_ITERS": 120}, timeout=300)
