@@ -280,15 +280,29 @@ struct Team {
 };
 
 // Memory of a team slot on this PE (round 6).  Predefined teams point into the base block; a
-// split team's own block (flag block + ring) and the imported blocks of its other members are
-// released by destroy.
+// split team uses one block of this PE's team-block pool (flag block + ring) and its co-members'
+// pool blocks, mapped here; destroy returns the block to the pool.
 struct TeamMem {
     uint32_t *flags[kMaxPes] = {};  // the team's flag block on world PE j, mapped here (members only)
     uint64_t *ring[kMaxPes] = {};   // the team's small-message ring on world PE j
-    void *own = nullptr;            // this PE's block of a split team
-    void *imported[kMaxPes] = {};   // members' blocks opened over IPC (split teams)
+    int pool_idx = -1;              // this PE's pool block of a split team
     char *fold_scratch = nullptr;   // in-place whole-array fold (kInplaceFoldBytes / p + 256 B)
     size_t fold_scratch_bytes = 0;
+};
+
+// Team blocks are pooled, never freed while the library is initialised: HIP keeps an allocation
+// that was exported for IPC allocated after hipFree until the process exits (8.25 MiB blocks,
+// 100 rounds: hipFree returned nothing after hipIpcGetMemHandle, every byte without it;
+// tools/ipc_leak_probe.py, profiles/r06/teams/), so a split / destroy cycle that allocated, exported
+// and freed a block leaked ~10 MiB per team and PE (the churn test caught 1460 MiB over 120
+// rounds).  A split takes a free pool block (zeroed) or exports a new one; destroy returns it.
+// The pool grows to the most split teams this PE was in at once.  Peers' pool blocks stay mapped
+// here once opened (keyed by PE and pool index), so re-splits reuse the mapping instead of
+// opening the handle again.
+struct PoolBlock {
+    uint32_t *ptr = nullptr;
+    hipIpcMemHandle_t handle{};
+    bool in_use = false;
 };
 
 constexpr long long kPhasedOff = std::numeric_limits<long long>::max();
@@ -342,7 +356,9 @@ struct State {
     int dev_id[kMaxPes] = {};            // world PE j's device, as an index into the job's devices
     TeamMem tmem[kMaxTeams];
     int teams_max = kTeamsMaxDefault;    // ISHMEM_TEAMS_MAX: slots [0, teams_max) are used
-    size_t team_block_bytes = 0;         // split teams' blocks this PE holds (get_param "flag_block_bytes")
+    size_t team_block_bytes = 0;         // pool blocks in use by split teams (get_param "flag_block_bytes")
+    std::vector<PoolBlock> team_pool;    // this PE's team blocks (PoolBlock)
+    std::map<std::pair<int, uint32_t>, void *> peer_pool;  // (world PE, its pool index) -> mapping here
     uint32_t *err_host = nullptr;  // host-mapped error words, one per team (+1: device API)
     uint32_t *err_dev = nullptr;
     // Host-mapped coherent [2][kMaxPes] u64 (same allocation as err_host): team_exchange's arrays.
@@ -1750,15 +1766,23 @@ int alloc_fold_scratch(State &s, int team, int p)
 void release_team_mem(State &s, int team)
 {
     TeamMem &m = s.tmem[team];
-    if (m.own || m.fold_scratch) (void) hipDeviceSynchronize();  // this PE's kernels are done with them
-    for (int j = 0; j < kMaxPes; ++j)
-        if (m.imported[j]) (void) hipIpcCloseMemHandle(m.imported[j]);
-    if (m.own) {
-        (void) hipFree(m.own);
+    if (m.pool_idx >= 0 || m.fold_scratch) (void) hipDeviceSynchronize();  // this PE's kernels are done with them
+    if (m.pool_idx >= 0 && m.pool_idx < (int) s.team_pool.size()) {
+        s.team_pool[(size_t) m.pool_idx].in_use = false;  // zeroed again when a split takes it
         s.team_block_bytes -= kTeamAllocBytes;
     }
-    if (m.fold_scratch) (void) hipFree(m.fold_scratch);
+    if (m.fold_scratch) (void) hipFree(m.fold_scratch);  // plain device memory, never exported
     m = TeamMem{};
+}
+
+// At finalize: the peers' pool blocks mapped here, then this PE's own pool.
+void release_team_pool(State &s)
+{
+    for (auto &kv : s.peer_pool) (void) hipIpcCloseMemHandle(kv.second);
+    s.peer_pool.clear();
+    for (PoolBlock &b : s.team_pool) (void) hipFree(b.ptr);
+    s.team_pool.clear();
+    s.team_block_bytes = 0;
 }
 
 // Device identity of every PE as small integers (PEs on one GPU share one), from the PCI bus ids
@@ -2412,6 +2436,7 @@ int ishmemi_c_finalize(void)
         release_team_mem(s, t);
         s.teams[t] = Team{};
     }
+    release_team_pool(s);
     (void) hipFree(s.dev_epochs);
     (void) hipFree(s.kern_ep);
     s.kern_ep = nullptr;
@@ -2623,12 +2648,14 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
     struct SplitRec {
         uint32_t ok, kind;
         uint64_t bytes;
+        uint32_t pool_idx, pad;
         hipIpcMemHandle_t handle;
     };
     static_assert(sizeof(SplitRec) <= kSplitRecBytes && kSplitRecBytes * kMaxPes + 256 <= kTeamScratchBytes,
                   "split exchange layout");
     const bool needs_mem = t.my_idx >= 0 && t.size > 1;
     uint32_t *block = nullptr;
+    int pidx = -1;  // this PE's pool block for the new team
     SplitRec mine{};
     std::string why;
     auto agree = [&](bool ok_here) -> int {  // AND over the parent; -1 if the reduce itself failed
@@ -2641,26 +2668,50 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
     bool ok = true;
     if (needs_mem) {
         std::lock_guard<std::mutex> lk(s.mu);
-        int kind = -1;
-        if (alloc_flag_mem(s, kTeamAllocBytes, s.flags_kind, true, s.npes > 1, &mine.handle, &block, &kind,
-                           "team_split_strided")) {
-            ok = false;
-            why = g_last_error;
-        } else if (alloc_fold_scratch(s, slot, t.size)) {
-            ok = false;
-            why = g_last_error;
+        for (size_t i = 0; i < s.team_pool.size() && pidx < 0; ++i)
+            if (!s.team_pool[i].in_use) pidx = (int) i;
+        if (pidx >= 0) {
+            // A pooled block still holds its last team's epochs: zero it before its handle goes
+            // out (the new team's launch words restart at 0, so an old epoch could read as arrived).
+            PoolBlock &b = s.team_pool[(size_t) pidx];
+            if (hipMemset(b.ptr, 0, kTeamAllocBytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                (void) hipGetLastError();
+                ok = false;
+                why = "team block reset failed";
+            }
         } else {
+            PoolBlock b;
+            int kind = -1;
+            if (alloc_flag_mem(s, kTeamAllocBytes, s.flags_kind, true, s.npes > 1, &b.handle, &b.ptr, &kind,
+                               "team_split_strided")) {
+                ok = false;
+                why = g_last_error;
+            } else {
+                s.team_pool.push_back(b);
+                pidx = (int) s.team_pool.size() - 1;
+            }
+        }
+        if (ok && alloc_fold_scratch(s, slot, t.size)) {
+            ok = false;
+            why = g_last_error;
+        }
+        if (pidx >= 0) {
+            PoolBlock &b = s.team_pool[(size_t) pidx];
+            b.in_use = true;
+            block = b.ptr;
+            mine.handle = b.handle;
+            mine.pool_idx = (uint32_t) pidx;
+        }
+        if (ok) {
             mine.ok = 1;
-            mine.kind = (uint32_t) kind;
+            mine.kind = (uint32_t) s.flags_kind;
             mine.bytes = kTeamAllocBytes;
         }
     }
-    auto undo = [&]() {
+    auto undo = [&]() {  // back to the state before the split (peers' mappings stay cached)
         std::lock_guard<std::mutex> lk(s.mu);
         TeamMem &m = s.tmem[slot];
-        for (int j = 0; j < kMaxPes; ++j)
-            if (m.imported[j]) (void) hipIpcCloseMemHandle(m.imported[j]);
-        if (block) (void) hipFree(block);
+        if (pidx >= 0) s.team_pool[(size_t) pidx].in_use = false;
         if (m.fold_scratch) (void) hipFree(m.fold_scratch);
         m = TeamMem{};
         block = nullptr;
@@ -2690,13 +2741,18 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
             }
             void *p = block;
             if (gpe != s.pe) {
-                if (hipIpcOpenMemHandle(&p, r.handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                const auto key = std::make_pair(gpe, r.pool_idx);
+                auto it = s.peer_pool.find(key);
+                if (it != s.peer_pool.end()) {
+                    p = it->second;  // mapped by an earlier split that used the same peer block
+                } else if (hipIpcOpenMemHandle(&p, r.handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
                     (void) hipGetLastError();
                     ok = false;
                     why = "hipIpcOpenMemHandle of member " + std::to_string(gpe) + "'s team block failed" + ipc_hint();
                     break;
+                } else {
+                    s.peer_pool[key] = p;
                 }
-                m.imported[gpe] = p;
             }
             m.flags[gpe] = (uint32_t *) p;
             m.ring[gpe] = (uint64_t *) ((char *) p + kTeamLLOffset);
@@ -2715,8 +2771,8 @@ int ishmemi_c_team_split_strided(int parent, int start, int stride, int size, in
         // mask of any parent containing one of them excludes it).
         if (t.my_idx >= 0) {
             s.teams[slot] = t;
-            s.tmem[slot].own = block;
-            if (block) s.team_block_bytes += kTeamAllocBytes;
+            s.tmem[slot].pool_idx = pidx;
+            if (pidx >= 0) s.team_block_bytes += kTeamAllocBytes;
         }
         // Launch words and device-API rows of the slot: zero them locally, then the parent sync
         // below orders the zeroing before any member's first collective on the new team (the
@@ -3274,6 +3330,8 @@ long long ishmemi_c_get_param(const char *name)
     // Flag memory this PE holds (base block + the split teams' blocks), against round 5's fixed
     // 16-slot block ("flag_block_bytes_round5").
     if (n == "flag_block_bytes") return s.initialized ? (long long) (kBaseAllocBytes + s.team_block_bytes) : 0;
+    // Team blocks this PE holds in its pool, in use or free for the next split (PoolBlock).
+    if (n == "flag_block_pool_bytes") return (long long) (s.team_pool.size() * kTeamAllocBytes);
     if (n == "flag_block_bytes_round5") return (long long) kRound5FlagBytes;
     for (int k = 0; k < 8; ++k)
         if (n == std::string("init_us_") + kInitPhase[k]) return (long long) s.init_us[k];
