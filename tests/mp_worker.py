@@ -243,7 +243,7 @@ def run(pe: int, npes: int, key: str, scenarios: list[str], q, env: dict | None 
             # Every PE's pool (<= 2 blocks) and the peers' blocks it maps (a few MiB of mapping each,
             # tools/ipc_leak_probe.py export_import) are one-time costs; the second half of the rounds,
             # with the pools warm, must not lose memory beyond a pool growing by one block.
-            allowance = npes * blocks * (10 << 20) + npes * (npes - 1) * blocks * (4 << 20) + (64 << 20)
+            allowance = npes * 2 * (10 << 20) + npes * (npes - 1) * 2 * (4 << 20) + (64 << 20)  # every PE's pool <= 2
             if free0 - free1 > allowance:
                 fails.append(f"pe{pe} churn: device free memory fell by {(free0 - free1) >> 20} MiB over {iters} "
                              f"rounds (pooled blocks allow {allowance >> 20} MiB)")
