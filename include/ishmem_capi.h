@@ -300,7 +300,8 @@ int ishmemi_c_register_device_ctx_slot(const void *host_shadow);
  * granule threshold and whole-array fold bound), "team_colocated" (1: every TEAM_WORLD member on
  * one GPU), "teams_max" (ISHMEM_TEAMS_MAX, default 64), "flag_block_bytes" (flag memory this PE
  * holds: the base block plus one block per split team it belongs to; "flag_block_bytes_round5" =
- * round 5's fixed 16-slot block, for comparison), "init_us_<phase>" (init's phases: hip, heap,
+ * round 5's fixed 16-slot block, for comparison; "flag_block_pool_bytes" = the exported team blocks
+ * this PE holds in its pool, in use or free for the next split), "init_us_<phase>" (init's phases: hip, heap,
  * flags, bootstrap, ipc_heap, ipc_flags, teams, total; printed under ISHMEM_DEBUG=2), "cu_count"
  * (compute units of this PE's device) and "device_share" (PEs of the job on this PE's device: 1
  * with one PE per GPU). */

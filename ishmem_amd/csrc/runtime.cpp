@@ -2409,6 +2409,11 @@ int ishmemi_c_finalize(void)
             s.peer_heap[j] = nullptr;
             s.peer_flags[j] = nullptr;
         }
+        // The peers' team-pool blocks too, before the barrier after which every PE frees its own
+        // exported memory (freeing an exported block while a peer still maps it is not something
+        // to depend on: tools/ipc_leak_probe.py's free-before-close case never completed).
+        for (auto &kv : s.peer_pool) (void) hipIpcCloseMemHandle(kv.second);
+        s.peer_pool.clear();
         s.boot.barrier(err);
         s.boot.detach();
     }
