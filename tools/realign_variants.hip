@@ -345,6 +345,45 @@ __global__ __launch_bounds__(64) void k_unal_sc(Args a)
     wt(uptr(a.d + wo), tid * 16u, acc);
 }
 
+// Round 6 (late): unaligned 16-B loads, one-wave workgroups, each workgroup U CONSECUTIVE 1 KiB
+// blocks, so the line straddling two blocks is re-read by the same wave (same CU, same L2) however
+// the workgroups are spread over the XCDs — the XCD grouping's effect without depending on the
+// dispatch order (which co-located PEs' grids break).  BURST: every block's loads issued before the
+// first store; otherwise block by block.
+template <int NS, int U, bool BURST>
+__global__ __launch_bounds__(64) void k_unalc(Args a)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i0 = (uint64_t) blockIdx.x * 64 * U;
+    if (i0 >= a.nitems) return;
+    const uint64_t wo = i0 * 16;
+    const auto r0 = rsrc(uptr(a.s[0] + a.k + wo)), r1 = rsrc(uptr(a.s[1] + a.k + wo));
+    const auto rd = rsrc(uptr(a.d + wo));
+    if constexpr (BURST) {
+        u32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t off = (u * 64 + tid) * 16u;
+            if (i0 + u * 64 + tid < a.nitems) {
+                x[u] = __builtin_amdgcn_raw_buffer_load_b128(r0, off, 0, kNT);
+                if (NS == 2) x[u] = addv(x[u], __builtin_amdgcn_raw_buffer_load_b128(r1, off, 0, kNT));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * 64 + tid < a.nitems) __builtin_amdgcn_raw_buffer_store_b128(x[u], rd, (u * 64 + tid) * 16u, 0, kSC);
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t off = (u * 64 + tid) * 16u;
+            if (i0 + u * 64 + tid >= a.nitems) break;
+            u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r0, off, 0, kNT);
+            if (NS == 2) x = addv(x, __builtin_amdgcn_raw_buffer_load_b128(r1, off, 0, kNT));
+            __builtin_amdgcn_raw_buffer_store_b128(x, rd, off, 0, kSC);
+        }
+    }
+}
+
 // The product's kernels with FaninArgs built as runtime.cpp plan_fanin builds them.
 static ishmemi::FaninArgs prod_args(const Args &a, int ns, bool aligned)
 {
@@ -467,29 +506,21 @@ int main(int argc, char **argv)
     CK(hipMemcpy(s0, h.data(), bytes + 4096, hipMemcpyHostToDevice));
     CK(hipMemcpy(s1, h1.data(), bytes + 4096, hipMemcpyHostToDevice));
     std::vector<Variant> vs = {
-        {"copy product aligned", 1, 64, 64, true, nullptr, 1},
-        {"copy product realign", 1, 512, 512, false, nullptr, 2},
-        {"copy wedge 512", 1, 512, 512, false, k_wedge<1, 512, false, false>},
-        {"copy wedge 256", 1, 256, 256, false, k_wedge<1, 256, false, false>},
-        {"copy wedge 1024", 1, 1024, 1024, false, k_wedge<1, 1024, false, false>},
-        {"copy wedge 64 xcd", 1, 64, 64, false, k_wedge<1, 64, false, true>},
-        {"copy unal 64 xcd", 1, 64, 64, false, k_unalw<1, 64, false, true>},
-        {"copy unal 512", 1, 512, 512, false, k_unalw<1, 512, false, false>},
         {"a+b product aligned", 2, 64, 64, true, nullptr, 1},
-        {"a+b product realign", 2, 512, 512, false, nullptr, 2},
-        {"a+b wedge 512", 2, 512, 512, false, k_wedge<2, 512, false, false>},
-        {"a+b wedge 512 serial", 2, 512, 512, false, k_wedge<2, 512, true, false>},
-        {"a+b wedge 256 serial", 2, 256, 256, false, k_wedge<2, 256, true, false>},
-        {"a+b wedge 64 xcd serial", 2, 64, 64, false, k_wedge<2, 64, true, true>},
         {"a+b unal 64 (rs now)", 2, 64, 64, false, k_unalw<2, 64, false, false>},
         {"a+b unal 64 xcd", 2, 64, 64, false, k_unalw<2, 64, false, true>},
-        {"a+b unal 64 xcd serial", 2, 64, 64, false, k_unalw<2, 64, true, true>},
-        {"a+b unal 512 serial", 2, 512, 512, false, k_unalw<2, 512, true, false>},
-        {"a+b unal 64 nt+sc", 2, 64, 64, false, k_unal_sc<2, false>},
-        {"a+b stshift 64 nt+sc", 2, 64, 64, false, k_stshift<2, false, true>},
-        {"a+b stshift 64 nt+nt", 2, 64, 64, false, k_stshift<2, false, false>},
-        {"a+b stshift 64 xcd nt+sc", 2, 64, 64, false, k_stshift<2, true, true>},
-        {"copy stshift 64", 1, 64, 64, false, k_stshift<1, false, false>},
+        {"a+b unalc 2 loop", 2, 64, 128, false, k_unalc<2, 2, false>},
+        {"a+b unalc 4 loop", 2, 64, 256, false, k_unalc<2, 4, false>},
+        {"a+b unalc 8 loop", 2, 64, 512, false, k_unalc<2, 8, false>},
+        {"a+b unalc 16 loop", 2, 64, 1024, false, k_unalc<2, 16, false>},
+        {"a+b unalc 2 burst", 2, 64, 128, false, k_unalc<2, 2, true>},
+        {"a+b unalc 4 burst", 2, 64, 256, false, k_unalc<2, 4, true>},
+        {"a+b unalc 8 burst", 2, 64, 512, false, k_unalc<2, 8, true>},
+        {"copy product aligned", 1, 64, 64, true, nullptr, 1},
+        {"copy product realign", 1, 512, 512, false, nullptr, 2},
+        {"copy unal 64", 1, 64, 64, false, k_unalw<1, 64, false, false>},
+        {"copy unalc 4 loop", 1, 64, 256, false, k_unalc<1, 4, false>},
+        {"copy unalc 8 burst", 1, 64, 512, false, k_unalc<1, 8, true>},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));

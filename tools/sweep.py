@@ -159,7 +159,6 @@ def main() -> None:
             print(f"{n * 4},{us:.2f},{n * 4 / 2**30 / (us * 1e-6):.2f},{int(ok)}", flush=True)
         n *= args.factor
     if args.phases and args.coll == "reduce":
-        import ctypes
         n = n // args.factor
         ish.set_param("phase_events", 1)
         for _ in range(2):
