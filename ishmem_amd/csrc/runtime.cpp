@@ -44,9 +44,10 @@ constexpr size_t kDevFlagBytes = (size_t) kMaxTeams * kDevFlagWordsPerTeam * 4;
 // Base flag block, allocated and IPC-exported at init (round 6): the predefined teams' flag blocks
 // (kernels.h kTeamFlagBytes each), the device-API flags of every slot, then the predefined teams'
 // small-message rings (kLLTeamBytes each), 256-B aligned.  A team created by a split gets a block
-// of its own (kTeamAllocBytes: flag block + ring), allocated and exchanged among its members at the
-// split and freed at destroy (TeamMem), so a PE holds (and peers map) blocks only for teams that
-// exist.  Round 5 reserved flag block + ring for 16 slots at init: 132 MiB per PE whatever the
+// of its own (kTeamAllocBytes: flag block + ring), taken from the PE's pool and exchanged among its
+// members at the split, returned to the pool at destroy (TeamMem, PoolBlock: HIP keeps an
+// IPC-exported allocation after hipFree, so blocks are reused and freed only at finalize); a PE
+// holds (and peers map) at most as many blocks as teams existed at once.  Round 5 reserved flag block + ring for 16 slots at init: 132 MiB per PE whatever the
 // teams (kRound5FlagBytes, for get_param "flag_block_bytes" comparisons).
 constexpr size_t kBaseDevOffset = (size_t) kPredefTeams * kTeamFlagBytes;
 constexpr size_t kBaseLLOffset = (kBaseDevOffset + kDevFlagBytes + 255) & ~(size_t) 255;
